@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — PPO experience+loss hot path throughput on MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--cpu-seconds S]
+
+One "step" = one PPOHotPath.step over one shard of synthetic rollouts (see
+trlx-t5_amd/step.py): policy+reference log-softmax-gather (experience), fused KL reward
++ GAE + whitening moments (+ RCCL all-reduce when N > 1), fused new-policy logprob + PPO
+gradient + dlogits write, value loss + stats.  Inputs are resident in HBM before timing.
+Weak scaling: every rank processes its own shard of the configuration's per-GPU batch;
+`value` = all ranks' tokens / max-over-ranks wall time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+  roofline      dominant kernel's algorithmic bytes / its average HIP-event time vs 8 TB/s
+  cpu_baseline  the oracle (op-for-op reference PyTorch path) on host cores, bounded sample
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "PPO experience+loss tokens/sec and % HBM roofline, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level table)
+
+CONFIGS = {
+    # name: (rows per GPU, response tokens, vocab, description)      BASELINE.json configs[]
+    "c2": (128, 48, 50257, "C2 GPT-2 sentiments PPO shape: 128 x 48 response tokens, vocab 50257, bf16 logits"),
+    "c3": (256, 48, 32128, "C3 T5-base seq2seq PPO: 256 rows/GPU x 48 decoder tokens (decoder-length masked), vocab 32128"),
+    "c4": (128, 128, 32128, "C4 UL2-20B rl_ul2 shape: 128 rows/GPU x 128 decoder tokens, vocab 32128, bf16 logits"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--no-timers", action="store_true", help="skip per-kernel HIP events")
+    return p.parse_args()
+
+
+def algorithmic_bytes(V, s, masked):
+    """Minimum HBM bytes per response token, per kernel."""
+    exp = 2 * V * s + 8 + 2 * 4                  # policy+ref rows, label, lp + ref_lp out
+    loss = 2 * V * s + 8 + 4 + 4 + 4 + (8 if masked else 0)  # row read + dlogits write, label, old_lp, adv, lp out
+    small = 4 * 4 + 4 * 2 + 4 + 4 * 2 + 4        # gae: values, lp, ref_lp, rewards/adv/ret out ...
+    stats = 4 * 6 + 4                            # loss elem: lp_new, v, old_lp, ov, adv, ret -> dv
+    return {"experience_lsm": exp, "loss_fused": loss, "step": exp + loss + small + stats}
+
+
+def make_inputs(torch, B, T, V, dev, seed, masked):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    bf = torch.bfloat16
+    logits = torch.randn(B, T, V, generator=g, device=dev, dtype=torch.float32).to(bf)
+    ref_logits = (logits.float() + 0.1 * torch.randn(B, T, V, generator=g, device=dev)).to(bf)
+    new_logits = (logits.float() + 0.05 * torch.randn(B, T, V, generator=g, device=dev)).to(bf)
+    labels = torch.randint(0, V, (B, T), generator=g, device=dev)
+    old_values = torch.randn(B, T, generator=g, device=dev)
+    values = old_values + 0.3 * torch.randn(B, T, generator=g, device=dev)
+    scores = torch.rand(B, generator=g, device=dev) * 24 - 12
+    lengths = mask = None
+    if masked:  # decoder lengths L ~ U{1..T}, zero right-padding (ppo_pipeline.py:47-65)
+        lengths = torch.randint(1, T + 1, (B,), generator=g, device=dev)
+        mask = (torch.arange(T, device=dev)[None, :] < lengths[:, None]).long()
+        old_values = old_values.masked_fill(mask == 0, 0)
+    torch.cuda.synchronize()
+    return dict(logits=logits, ref_logits=ref_logits, new_logits=new_logits, labels=labels,
+                old_values=old_values, values=values, scores=scores, lengths=lengths, mask=mask)
+
+
+def cpu_baseline(torch, T, V, seconds):
+    """Oracle (reference PyTorch ops, native bf16 like the T5/UL2 path) on host cores."""
+    from oracle import ppo_oracle as orc
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    Bs = 8
+    g = torch.Generator().manual_seed(123)
+    bf = torch.bfloat16
+    logits = torch.randn(Bs, T, V, generator=g).to(bf)
+    ref_logits = (logits.float() + 0.1 * torch.randn(Bs, T, V, generator=g)).to(bf)
+    new_logits = (logits.float() + 0.05 * torch.randn(Bs, T, V, generator=g)).to(bf)
+    labels = torch.randint(0, V, (Bs, T), generator=g)
+    old_values = torch.randn(Bs, T, generator=g).to(bf)
+    values = (old_values.float() + 0.3 * torch.randn(Bs, T, generator=g)).to(bf)
+    scores = torch.rand(Bs, generator=g) * 24 - 12
+    toks, t0 = 0, time.perf_counter()
+    while True:
+        orc.ppo_step_reference(logits, ref_logits, new_logits, labels, old_values, values, scores, kl_coef=0.05)
+        toks += Bs * T
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": toks / el, "unit": "tokens/s", "cores": cores, "kind": "port",
+            "sample": f"{toks // (Bs * T)} steps of {Bs}x{T}x{V} bf16 (oracle.ppo_step_reference: reference ops "
+                      f"incl. autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__
+    P = __graft_entry__.load_package()
+    P.load_library()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, T, V, desc = CONFIGS[args.config]
+    masked = args.config == "c3"
+    x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked)
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05)
+
+    def step():
+        return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],
+                       x["values"], x["scores"], lengths=x["lengths"], mask=x["mask"])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if not args.no_timers:
+        hp.timers = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, dist.ReduceOp.MAX)
+        elapsed = float(t)
+
+    # per-kernel average durations (HIP events on the launch stream, timed region only)
+    kern_ms = {}
+    if hp.timers:
+        for name, evs in hp.timers.items():
+            kern_ms[name] = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    tokens = B * T
+    ab = algorithmic_bytes(V, 2, masked)
+    roof = None
+    if kern_ms:
+        dom = max(("experience_lsm", "loss_fused"), key=lambda k: kern_ms.get(k, 0.0))
+        ach = ab[dom] * tokens / (kern_ms[dom] * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                rec = json.load(f)
+            traffic = rec.get(args.config, {}).get(dom)
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
+                "bytes_per_launch": ab[dom] * tokens, "avg_launch_us": round(kern_ms[dom] * 1e3, 2),
+                "kernels_avg_us": {k: round(v * 1e3, 2) for k, v in kern_ms.items()},
+                "step_frac": round(ab["step"] * tokens / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(torch, T, V, args.cpu_seconds)
+        ms = elapsed / args.steps * 1e3
+        out = {
+            "metric": METRIC,
+            "value": round(world * tokens * args.steps / elapsed, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world, "seq_len": T, "vocab": V,
+                       "logits_dtype": "bf16", "tokens_per_gpu_step": tokens, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

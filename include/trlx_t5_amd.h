@@ -1,0 +1,176 @@
+/*
+ * trlx_t5_amd.h — C ABI of the MI355X-native PPO experience-and-loss hot path.
+ *
+ * Test-free, torch-free boundary: plain device pointers, int64 sizes/strides (in
+ * ELEMENTS), dtype enums, scalar hyper-parameters by value and the caller's stream
+ * (a hipStream_t passed as void*; NULL = the default stream).  Every entry point is
+ * stream-ordered and asynchronous: no host synchronisation, no allocation, no pointer
+ * retained past the call.  All return an int status (TRLX_OK = 0); on failure
+ * trlx_last_error() returns a thread-local message.
+ *
+ * The reference (danyang-rainbow/trlx-t5) has no FFI layer: its hot path is plain
+ * Python functions.  Each entry point below names the reference function (file:line,
+ * into the reference repo) whose arithmetic it replaces; the Python drop-in that binds
+ * them (trlx-t5_amd/) keeps those functions' names and signatures.
+ *
+ * Layout conventions
+ *   logits   : [B, T, V], row (b, t) starts at  logits + b*sb + t*st,  V contiguous.
+ *   labels   : int64, element (b, t) at labels + b*lb + t*lt, in [0, V) (out of range
+ *              produces NaN, never an out-of-bounds read).
+ *   [B, T] per-token vectors (logprobs, values, rewards, advantages, ...) : contiguous.
+ *   dtype    : TRLX_F32 or TRLX_BF16 (logits / per-token vectors), arithmetic is fp32
+ *              with fp64 accumulation for batch statistics.
+ */
+#ifndef TRLX_T5_AMD_H
+#define TRLX_T5_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRLX_ABI_VERSION 1
+
+typedef enum {
+    TRLX_F32 = 0,
+    TRLX_BF16 = 1,
+    TRLX_I64 = 2,   /* masks / lengths only */
+} trlx_dtype;
+
+typedef enum {
+    TRLX_OK = 0,
+    TRLX_ERR_SHAPE = 1,   /* bad size / shape */
+    TRLX_ERR_STRIDE = 2,  /* unsupported stride */
+    TRLX_ERR_DTYPE = 3,   /* unsupported dtype */
+    TRLX_ERR_LAUNCH = 4,  /* kernel launch failed */
+    TRLX_ERR_ARG = 5,     /* NULL pointer / bad scalar */
+} trlx_status;
+
+/* Number of fp64 slots per partial-statistics record (see trlx_gae_scan). */
+#define TRLX_MOMENT_SLOTS 4     /* {sum x, sum x^2, count, sum mask} */
+/* Number of fp32 slots written by trlx_ppo_loss_finalize (order = stats keys of
+ * PPOConfig.loss, ppo_models.py:182-198, after losses). */
+#define TRLX_PPO_STATS 13
+/* Number of fp64 partial-sum slots per block of trlx_ppo_loss_elem. */
+#define TRLX_PPO_PARTIAL_SLOTS 16
+
+int trlx_abi_version(void);
+const char* trlx_last_error(void);
+
+/* ---------------------------------------------------------------- A1
+ * logprobs_from_logits forward — replaces trlx/utils/modeling.py:37-41
+ * (F.log_softmax over V + gather at labels), fused in one pass over each row; the
+ * [B,T,V] log-softmax is never materialised.
+ * Up to two logits tensors of identical shape/strides/dtype are processed in one launch
+ * (x1 may be NULL): the experience step's policy and reference logits
+ * (ppo_orchestrator.py:154-155).  out_lp{0,1}: [B,T] of out_dtype.  out_lse{0,1}:
+ * optional fp32 [B,T] log-sum-exp saved for the backward. */
+int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype,
+                        int64_t B, int64_t T, int64_t V, int64_t sb, int64_t st,
+                        const int64_t* labels, int64_t lb, int64_t lt,
+                        void* out_lp0, void* out_lp1, int out_dtype,
+                        float* out_lse0, float* out_lse1, void* stream);
+
+/* ---------------------------------------------------------------- A1 backward
+ * Autograd of modeling.py:39-40 (log_softmax_backward of the gathered one-hot):
+ *   dx[b,t,j] = g[b,t] * ([j == y] - exp(x[b,t,j] - lse[b,t]))
+ * grad: [B,T] of grad_dtype; dx row (b,t) at dx + b*dsb + t*dst, same dtype as x.  One
+ * read of the row and one write, no reduction (lse from the forward). */
+int trlx_lsm_gather_bwd(const void* x, int dtype, int64_t B, int64_t T, int64_t V,
+                        int64_t sb, int64_t st, const int64_t* labels, int64_t lb, int64_t lt,
+                        const float* lse, const void* grad, int grad_dtype,
+                        void* dx, int64_t dsb, int64_t dst, void* stream);
+
+/* ---------------------------------------------------------------- A2
+ * KL-penalised reward — replaces ppo_orchestrator.py:164-167:
+ *   r[b,t] = -beta * (lp[b,t] - ref_lp[b,t]);  r[b, T-1] += scores[b]
+ * (with lengths != NULL the score goes to column lengths[b]-1 and columns >= lengths[b]
+ * are padding: reward 0).  lp/ref_lp: [B,T] of in_dtype; scores fp32 [B] or NULL. */
+int trlx_kl_penalty_rewards(const void* lp, const void* ref_lp, int in_dtype,
+                            int64_t B, int64_t T, float beta, const float* scores,
+                            const int64_t* lengths, void* rewards, int out_dtype, void* stream);
+
+/* ---------------------------------------------------------------- A5 (+A2 fused, +A3 partials)
+ * GAE reverse scan — replaces ppo_models.py:121-136 (the per-t Python loop):
+ *   delta_t = r_t + gamma*V_{t+1} - V_t   (V_T := 0);   A_t = delta_t + (gamma*lam)*A_{t+1}
+ *   returns = A + V  (unwhitened A)
+ * values / rewards: [B, T] of dtype (rows contiguous, row stride T); columns
+ * [0, Teff) are used (Teff = response_length).  If lp != NULL the rewards are not read
+ * but computed in-kernel from (lp, ref_lp, neg_beta, scores) exactly as
+ * trlx_kl_penalty_rewards does (fp32 lp/ref_lp [B,T]) and, if rew_out != NULL, stored.
+ * lengths (nullable): positions t >= lengths[b] are padding (value/reward read as 0).
+ * Outputs: adv_raw fp32 [B,Teff] (unwhitened), ret [B,Teff] of ret_dtype, and per-block
+ * partial moments of adv_raw: partials[blk*4 + {0,1,2,3}] = {sum A, sum A^2, count,
+ * sum mask} (mask: int64 [B,Teff] loss mask, NULL = all ones).
+ * trlx_gae_num_blocks(B, Teff) tells how many partial records are written. */
+int64_t trlx_gae_num_blocks(int64_t B, int64_t Teff);
+int trlx_gae_scan(const void* values, const void* rewards, int dtype, int64_t B, int64_t T,
+                  int64_t Teff, float gamma, float lam,
+                  const float* lp, const float* ref_lp, float neg_beta, const float* scores,
+                  const int64_t* lengths, const int64_t* mask,
+                  float* adv_raw, void* ret, int ret_dtype, void* rew_out, int rew_dtype,
+                  double* partials, void* stream);
+
+/* ---------------------------------------------------------------- A3 helpers
+ * Partial moments of an arbitrary contiguous tensor (for whiten / get_global_statistics,
+ * modeling.py:9-34, and RunningMoments, :72-104).  trlx_moments_num_blocks(n) records. */
+int64_t trlx_moments_num_blocks(int64_t n);
+int trlx_moments_partial(const void* x, int dtype, int64_t n, double* partials, void* stream);
+/* (dtype may also be TRLX_I64 here, e.g. to sum a loss mask.) */
+/* Reduce nblk partial records (fixed order, deterministic) into stats[4]. */
+int trlx_moments_finalize(const double* partials, int64_t nblk, double* stats, void* stream);
+
+/* ---------------------------------------------------------------- A4
+ * whiten — replaces modeling.py:24-34:  out = (x - mu) * rsqrt(var + 1e-8) [+ mu]
+ * mu, var from stats[4] = {sum, sumsq, count, .}: var = M2/count (biased, the
+ * distributed branch) or M2/(count-1) (unbiased, torch.var_mean branch). */
+int trlx_whiten_apply(const void* x, int dtype, int64_t n, const double* stats, int unbiased,
+                      int shift_mean, void* out, int out_dtype, void* stream);
+
+/* ---------------------------------------------------------------- A1+A4+A6 fused (loss side)
+ * One pass over each policy-logits row: lse, lp = x[y] - lse, then the closed-form
+ * per-token gradient of PPOConfig.loss's policy term (ppo_models.py:165-177 with torch's
+ * max-tie and clamp-bound rules) and the row's dlogits = g * (onehot - softmax), written
+ * once.  Advantages are whitened on the fly from adv_raw + stats (stats == NULL: adv is
+ * used as given).  mask: int64 [B,T] or NULL (all ones); msum: device fp64 scalar (NULL:
+ * use msum_host).  Outputs: lp_out fp32 [B,T]; dx (row (b,t) at dx + b*dsb + t*dst, dtype
+ * of x). */
+int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_t T, int64_t V,
+                          int64_t sb, int64_t st, const int64_t* labels, int64_t lb, int64_t lt,
+                          const void* old_lp, int old_dtype, const float* adv,
+                          const double* stats, int unbiased, const int64_t* mask,
+                          const double* msum, double msum_host, float cliprange,
+                          float* lp_out, void* dx, int64_t dsb, int64_t dst, void* stream);
+
+/* ---------------------------------------------------------------- A6
+ * PPOConfig.loss (ppo_models.py:141-199) over [B,T] vectors.  Pass 1 (elementwise,
+ * many blocks): per-token value/policy terms, gradients d loss/d lp (dlp, optional) and
+ * d loss/d values (dv, optional) and fp64 partial sums (TRLX_PPO_PARTIAL_SLOTS per
+ * block).  Pass 2 (one block, fixed order): loss[1] and stats[TRLX_PPO_STATS] fp32 in the
+ * order total_loss, policy_loss, value_loss, mean_old_values, var_old_values,
+ * mean_values, values_error, values_clipfrac, approx_kl, policy_clipfrac,
+ * returns_mean, returns_var, ratio.
+ * lp, values, old_lp, old_values, adv, returns: [n] of the respective dtypes (adv fp32,
+ * optionally whitened on the fly from adv_stats); mask int64 [n] or NULL. */
+int64_t trlx_ppo_loss_num_blocks(int64_t n);
+int trlx_ppo_loss_elem(int64_t n, const void* lp, int lp_dtype, const void* values, int v_dtype,
+                       const void* old_lp, int olp_dtype, const void* old_values, int ov_dtype,
+                       const void* adv, int a_dtype,
+                       const double* adv_stats, int unbiased, const void* returns,
+                       int r_dtype, const int64_t* mask, const double* msum, double msum_host,
+                       float cliprange, float cliprange_value, float vf_coef,
+                       void* dlp, void* dv, int g_dtype, double* partials, void* stream);
+int trlx_ppo_loss_finalize(const double* partials, int64_t nblk, int64_t n,
+                           const double* msum, double msum_host, float vf_coef,
+                           float* loss, float* stats, void* stream);
+
+/* ---------------------------------------------------------------- autograd plumbing
+ * out[i] = x[i] * (*scale) for i < n (scale: device fp32 scalar, e.g. a backward's
+ * grad_output).  In place (out == x) it is skipped entirely when *scale == 1. */
+int trlx_scale_by(const void* x, void* out, int dtype, int64_t n, const float* scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRLX_T5_AMD_H */

@@ -1,0 +1,376 @@
+"""GPU parity: every HIP kernel, called through the C ABI (via the drop-in Python surface
+or directly with _lib.call), against (a) the golden fixtures produced by the reference
+and (b) the CPU oracle (oracle/ppo_oracle.py, pinned to those fixtures) on the same
+seeded inputs.
+
+Tolerances (BASELINE.json north star):
+  gather indices / masks / counts       bit-exact
+  fp32 quantities                       rtol 1e-5 (+ small atol for near-zero elements)
+  bf16 outputs vs the reference's bf16  rtol 2e-2 (logprobs)
+  bf16 *inputs*: kernels compute in fp32, so they are compared at rtol 1e-5 against the
+  oracle evaluated in fp32 on the same bf16-quantised inputs (SURVEY §8c precision rule).
+"""
+import numpy as np
+import pytest
+import torch
+
+import trlx_t5_amd as P
+from trlx_t5_amd import _lib
+from golden_util import T, is_bf16
+from oracle import ppo_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+RT32 = dict(rtol=1e-5, atol=1e-5)
+
+
+def cuda(t):
+    return t.to(DEV)
+
+
+def lp_fp32_via_abi(logits, labels):
+    """lsm_gather_fwd with an fp32 output regardless of the logits dtype (C ABI direct)."""
+    x = cuda(logits).contiguous()
+    y = cuda(labels).contiguous()
+    B, Tn, V = x.shape
+    out = torch.empty((B, Tn), dtype=torch.float32, device=DEV)
+    lse = torch.empty((B, Tn), dtype=torch.float32, device=DEV)
+    _lib.call("trlx_lsm_gather_fwd", x.data_ptr(), None, _lib.dtype_code(x), B, Tn, V, x.stride(0), x.stride(1),
+              y.data_ptr(), y.stride(0), y.stride(1), out.data_ptr(), None, _lib.F32, lse.data_ptr(), None,
+              _lib.stream_of(x))
+    return out.cpu(), lse.cpu()
+
+
+# ------------------------------------------------------------------ A1 logprobs_from_logits
+CASES_LSM = ["small_f32", "small_bf16", "peaked_f32", "wide50257_f32", "wide50257_bf16", "wide32128_bf16"]
+
+
+@pytest.mark.parametrize("case", CASES_LSM)
+def test_logprobs_golden(golden, case):
+    z = golden("lsm_gather")
+    x, y = T(z[f"{case}/logits"]), T(z[f"{case}/labels"])
+    want = T(z[f"{case}/lp"])
+    got = P.logprobs_from_logits(cuda(x), cuda(y)).cpu()
+    assert got.dtype == x.dtype
+    if x.dtype == torch.bfloat16:
+        torch.testing.assert_close(got.float(), want.float(), rtol=2e-2, atol=2e-2)
+    else:
+        torch.testing.assert_close(got, want, **RT32)
+    # fp32 arithmetic on the (quantised) inputs vs the fp32 oracle
+    lp32, lse = lp_fp32_via_abi(x, y)
+    torch.testing.assert_close(lp32, orc.logprobs_from_logits(x.float(), y), **RT32)
+    torch.testing.assert_close(lse, torch.logsumexp(x.float(), -1), **RT32)
+
+
+@pytest.mark.parametrize("case", CASES_LSM)
+def test_logprobs_backward_golden(golden, case):
+    z = golden("lsm_gather")
+    x, y, w = T(z[f"{case}/logits"]), T(z[f"{case}/labels"]), T(z[f"{case}/w"])
+    xg = cuda(x).requires_grad_(True)
+    lp = P.logprobs_from_logits(xg, cuda(y))
+    (lp * cuda(w)).sum().backward()
+    got = xg.grad.cpu()
+    assert got.dtype == x.dtype and got.shape == x.shape
+    # fp32 oracle on the quantised inputs (the reference's bf16 autograd rounds its own
+    # log-softmax to bf16 first; the fixture is checked with a bf16-ulp tolerance)
+    xf = x.float().requires_grad_(True)
+    (orc.logprobs_from_logits(xf, y) * w.float()).sum().backward()
+    if x.dtype == torch.bfloat16:
+        torch.testing.assert_close(got.float(), xf.grad, rtol=1e-2, atol=1e-6)
+        torch.testing.assert_close(got.float(), T(z[f"{case}/dlogits"]).float(), rtol=2e-2, atol=2e-4)
+    else:
+        torch.testing.assert_close(got, xf.grad, **RT32)
+        torch.testing.assert_close(got, T(z[f"{case}/dlogits"]), **RT32)
+
+
+@pytest.mark.parametrize("V", [1, 5, 7, 8, 9, 37, 255, 4097, 32128, 50257])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_logprobs_vocab_edges(V, dt):
+    """Head/tail peeling: every row start phase (odd V => rows start at every 2-B offset)."""
+    g = torch.Generator().manual_seed(V)
+    B, Tn = 3, 5
+    x = (torch.randn(B, Tn, V, generator=g) * 3).to(dt)
+    y = torch.randint(0, V, (B, Tn), generator=g)
+    y[0, 0], y[-1, -1] = 0, V - 1
+    lp32, _ = lp_fp32_via_abi(x, y)
+    torch.testing.assert_close(lp32, orc.logprobs_from_logits(x.float(), y), **RT32)
+    xg = cuda(x).requires_grad_(True)
+    P.logprobs_from_logits(xg, cuda(y)).float().sum().backward()
+    xf = x.float().requires_grad_(True)
+    orc.logprobs_from_logits(xf, y).sum().backward()
+    tol = dict(rtol=1e-2, atol=1e-6) if dt == torch.bfloat16 else RT32
+    torch.testing.assert_close(xg.grad.float().cpu(), xf.grad, **tol)
+
+
+def test_logprobs_strided_causal_view():
+    """logits[:, :-1] / tokens[:, 1:] (the causal caller pattern) without copies; the grad
+    buffer keeps the view's strides and phase."""
+    g = torch.Generator().manual_seed(7)
+    B, L, V = 3, 6, 1001
+    full = torch.randn(B, L, V, generator=g).to(torch.bfloat16)
+    tok = torch.randint(0, V, (B, L), generator=g)
+    xf = cuda(full).requires_grad_(True)
+    lp = P.logprobs_from_logits(xf[:, :-1], cuda(tok)[:, 1:])
+    lp.float().sum().backward()
+    ref_x = full.float().requires_grad_(True)
+    ref = orc.logprobs_from_logits(ref_x[:, :-1], tok[:, 1:])
+    ref.sum().backward()
+    torch.testing.assert_close(lp.float().cpu(), ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(xf.grad.float().cpu(), ref_x.grad, rtol=1e-2, atol=1e-6)
+    # 2-D [N, V] input
+    lp2 = P.logprobs_from_logits(cuda(full.reshape(-1, V)), cuda(tok.reshape(-1)))
+    torch.testing.assert_close(lp2.float().cpu(), orc.logprobs_from_logits(full.float().reshape(-1, V),
+                                                                            tok.reshape(-1)), rtol=2e-2, atol=2e-2)
+
+
+def test_logprobs_bad_label_is_nan_not_oob():
+    x = torch.randn(1, 3, 100)
+    y = torch.tensor([[0, 100, -1]])
+    lp32, _ = lp_fp32_via_abi(x, y)
+    assert torch.isfinite(lp32[0, 0]) and torch.isnan(lp32[0, 1]) and torch.isnan(lp32[0, 2])
+
+
+def test_logprobs_empty_and_determinism():
+    x = cuda(torch.randn(0, 4, 50))
+    y = cuda(torch.zeros(0, 4, dtype=torch.long))
+    assert P.logprobs_from_logits(x, y).shape == (0, 4)
+    g = torch.Generator().manual_seed(1)
+    x = cuda(torch.randn(16, 8, 50257, generator=g).to(torch.bfloat16))
+    y = cuda(torch.randint(0, 50257, (16, 8), generator=g))
+    a, b = P.logprobs_from_logits(x, y), P.logprobs_from_logits(x, y)
+    assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------------ A2 KL reward
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_kl_rewards_golden(golden, dt):
+    z = golden("kl_reward")
+    k = f"{dt}/none"
+    lp, rlp = T(z[f"{k}/lp"]), T(z[f"{k}/ref_lp"])
+    s = T(z[f"{k}/scores_out"])
+    got = P.kl_penalty_rewards(cuda(lp), cuda(rlp), float(z[f"{dt}/beta"]), cuda(s)).cpu()
+    want = T(z[f"{k}/rewards"])
+    if dt == "bf16":
+        # fp32 arithmetic on the same bf16 logprobs, rounded once to bf16
+        ref32 = orc.kl_penalty_rewards(lp.float(), rlp.float(), 0.05, s)
+        torch.testing.assert_close(got.float(), ref32, rtol=1e-2, atol=1e-4)
+    else:
+        torch.testing.assert_close(got, want, **RT32)
+
+
+def test_kl_rewards_lengths():
+    g = torch.Generator().manual_seed(3)
+    B, Tn = 6, 11
+    lp, rlp = torch.randn(B, Tn, generator=g), torch.randn(B, Tn, generator=g)
+    s = torch.randn(B, generator=g)
+    L = torch.tensor([11, 1, 5, 10, 3, 11])
+    got = P.kl_penalty_rewards(cuda(lp), cuda(rlp), 0.05, cuda(s), lengths=cuda(L)).cpu()
+    torch.testing.assert_close(got, orc.kl_penalty_rewards(lp, rlp, 0.05, s, L), **RT32)
+
+
+# ------------------------------------------------------------------ A3/A4 whiten
+@pytest.mark.parametrize("name", ["f32", "bf16", "f32_big"])
+def test_whiten_golden(golden, name):
+    z = golden("whiten")
+    xs = T(z[f"{name}/xs"])
+    for fn_kwargs, key in [({}, "nodist"), ({"shift_mean": False}, "nodist_noshift"),
+                           ({"distributed": False}, "nodist_disabled")]:
+        got = P.whiten(cuda(xs), **fn_kwargs).cpu()
+        assert got.dtype == xs.dtype
+        if xs.dtype == torch.bfloat16:
+            ref32 = orc.whiten(xs.float(), **fn_kwargs)
+            torch.testing.assert_close(got.float(), ref32, rtol=1e-2, atol=1e-2)
+        else:
+            torch.testing.assert_close(got, T(z[f"{name}/{key}"]), **RT32)
+
+
+def test_moments_and_global_statistics_single_process():
+    g = torch.Generator().manual_seed(5)
+    xs = torch.randn(300, 7, generator=g) * 2 + 1
+    st = P.moments(cuda(xs)).cpu()
+    assert st[2].item() == xs.numel()
+    torch.testing.assert_close(st[0], xs.double().sum(), rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(st[1], (xs.double() ** 2).sum(), rtol=1e-12, atol=1e-9)
+    m = torch.randint(0, 2, (300, 7))
+    assert P.moments(cuda(m)).cpu()[0].item() == m.sum().item()
+
+
+def test_running_moments_kat_device(golden):
+    z = golden("host_state")
+    rm = P.RunningMoments()
+    for i in range(4):
+        a = T(z[f"rm/{i}/in"]).float()
+        bm, bs = rm.update(cuda(a))
+        assert float(bm) == pytest.approx(float(z[f"rm/{i}/batch_mean"]), rel=1e-6, abs=1e-6)
+        assert float(bs) == pytest.approx(float(z[f"rm/{i}/batch_std"]), rel=1e-6)
+        assert rm.std == pytest.approx(float(z[f"rm/{i}/std"]), rel=1e-6)
+
+
+# ------------------------------------------------------------------ A5 GAE
+def test_gae_golden_all_cases(golden):
+    z = golden("gae")
+    keys = sorted({k.split("/")[0] for k in z.files})
+    for k in keys:
+        v, r = T(z[f"{k}/values"]), T(z[f"{k}/rewards"])
+        cfg = P.PPOConfig(gamma=float(z[f"{k}/gamma"]), lam=float(z[f"{k}/lam"]))
+        whit = k.endswith("_w1")
+        adv, ret = cfg.get_advantages_and_returns(cuda(v), cuda(r), v.shape[1], use_whitening=whit)
+        adv, ret = adv.cpu(), ret.cpu()
+        assert adv.dtype == v.dtype and ret.dtype == v.dtype
+        if v.dtype == torch.float32:
+            torch.testing.assert_close(adv, T(z[f"{k}/adv"]), **RT32, msg=k)
+            torch.testing.assert_close(ret, T(z[f"{k}/ret"]), **RT32, msg=k)
+        else:
+            a32, r32 = orc.gae(v.float(), r.float(), v.shape[1], cfg.gamma, cfg.lam, use_whitening=whit)
+            torch.testing.assert_close(adv.float(), a32, rtol=1e-2, atol=1e-2, msg=k)
+            torch.testing.assert_close(ret.float(), r32, rtol=1e-2, atol=1e-2, msg=k)
+            # fp32 raw path (no final rounding): 1e-5
+            araw, rraw, _ = cfg.gae_raw(cuda(v), cuda(r), v.shape[1])
+            a32n, _ = orc.gae(v.float(), r.float(), v.shape[1], cfg.gamma, cfg.lam, use_whitening=False)
+            torch.testing.assert_close(araw.cpu(), a32n, **RT32, msg=k)
+
+
+@pytest.mark.parametrize("B,Tn", [(1, 1), (3, 1), (130, 48), (1024, 128), (7, 300)])
+def test_gae_shapes(B, Tn):
+    g = torch.Generator().manual_seed(B * 1000 + Tn)
+    v, r = torch.randn(B, Tn, generator=g), torch.randn(B, Tn, generator=g)
+    cfg = P.PPOConfig(gamma=0.99)
+    adv, ret = cfg.get_advantages_and_returns(cuda(v), cuda(r), Tn, use_whitening=B * Tn > 1)
+    a, rr = orc.gae(v, r, Tn, 0.99, 0.95, use_whitening=B * Tn > 1)
+    torch.testing.assert_close(ret.cpu(), rr, **RT32)
+    torch.testing.assert_close(adv.cpu(), a, rtol=1e-5, atol=1e-4)
+
+
+# ------------------------------------------------------------------ A6 PPO loss
+LOSS_CASES = ["random", "masked", "ties", "wide_ratio", "bf16", "vf_coef"]
+
+
+@pytest.mark.parametrize("case", LOSS_CASES)
+def test_ppo_loss_golden(golden, case):
+    z = golden("ppo_loss")
+    g = {n: T(z[f"{case}/{n}"]) for n in ("lp", "olp", "v", "ov", "adv", "ret", "mask")}
+    cfg = P.PPOConfig(vf_coef=float(z[f"{case}/vf_coef"]))
+    lp = cuda(g["lp"]).requires_grad_(True)
+    v = cuda(g["v"]).requires_grad_(True)
+    loss, stats = cfg.loss(lp, v, cuda(g["olp"]), cuda(g["ov"]), cuda(g["adv"]), cuda(g["ret"]), cuda(g["mask"]))
+    loss.backward()
+    assert set(stats) == set(P.STATS_KEYS)
+    for k in ("losses/total_loss", "losses/policy_loss", "losses/value_loss", "policy/approx_kl",
+              "policy/clipfrac"):
+        assert isinstance(stats[k], float)
+    if g["lp"].dtype == torch.bfloat16:
+        # fp32 oracle on the bf16-quantised inputs
+        lpf = g["lp"].float().requires_grad_(True)
+        vf = g["v"].float().requires_grad_(True)
+        rloss, rstats = orc.ppo_loss(lpf, vf, *(g[n].float() for n in ("olp", "ov", "adv", "ret")), g["mask"],
+                                     vf_coef=cfg.vf_coef)
+        rloss.backward()
+        want_loss, want_glp, want_gv = rloss.detach(), lpf.grad, vf.grad
+        want_stats = {k: float(val) for k, val in rstats.items()}
+        gtol = dict(rtol=1e-2, atol=1e-4)  # grads are returned in bf16 (input dtype)
+    else:
+        want_loss, want_glp, want_gv = T(z[f"{case}/loss"]), T(z[f"{case}/grad_lp"]), T(z[f"{case}/grad_v"])
+        want_stats = {k: float(z[f"{case}/stats/{k}"]) for k in P.STATS_KEYS}
+        gtol = RT32
+    torch.testing.assert_close(loss.detach().cpu().float(), want_loss.float(), **RT32)
+    torch.testing.assert_close(lp.grad.cpu().float(), want_glp.float(), **gtol)
+    torch.testing.assert_close(v.grad.cpu().float(), want_gv.float(), **gtol)
+    for k in P.STATS_KEYS:
+        assert float(stats[k]) == pytest.approx(want_stats[k], rel=1e-5, abs=1e-6), k
+
+
+@pytest.mark.parametrize("dt", ["float32", "bfloat16"])
+def test_loss_from_logits_chain_golden(golden, dt):
+    """Fused A1+A6 (one pass over each logits row) == logprobs_from_logits -> loss -> backward."""
+    z = golden("ppo_loss")
+    k = f"chain_{dt}"
+    x, y = T(z[f"{k}/logits"]), T(z[f"{k}/labels"])
+    olp, ov, adv, ret, v = (T(z[f"{k}/{n}"]) for n in ("olp", "ov", "adv", "ret", "v"))
+    cfg = P.PPOConfig()
+    xg = cuda(x).requires_grad_(True)
+    vg = cuda(v).requires_grad_(True)
+    loss, stats, lp_new = cfg.loss_from_logits(xg, vg, cuda(y), cuda(olp), cuda(ov), cuda(adv), cuda(ret))
+    loss.backward()
+    # oracle in fp32 on the same (quantised) inputs
+    xf = x.float().requires_grad_(True)
+    vf = v.float().requires_grad_(True)
+    lpf = orc.logprobs_from_logits(xf, y)
+    rloss, rstats = orc.ppo_loss(lpf, vf, olp.float(), ov.float(), adv.float(), ret.float(),
+                                 torch.ones(y.shape, dtype=torch.long))
+    rloss.backward()
+    torch.testing.assert_close(lp_new.cpu(), lpf.detach(), **RT32)
+    torch.testing.assert_close(loss.detach().cpu(), rloss.detach(), **RT32)
+    if x.dtype == torch.float32:
+        torch.testing.assert_close(xg.grad.cpu(), xf.grad, **RT32)
+        torch.testing.assert_close(xg.grad.cpu(), T(z[f"{k}/dlogits"]), **RT32)
+        torch.testing.assert_close(vg.grad.cpu(), T(z[f"{k}/grad_v"]), **RT32)
+    else:
+        torch.testing.assert_close(xg.grad.cpu().float(), xf.grad, rtol=1e-2, atol=1e-7)
+        torch.testing.assert_close(vg.grad.cpu().float(), vf.grad, rtol=1e-2, atol=1e-5)
+    for key in P.STATS_KEYS:
+        assert float(stats[key]) == pytest.approx(float(rstats[key]), rel=1e-5, abs=1e-6), key
+
+
+# ------------------------------------------------------------------ the fused step (bench path)
+def _step_inputs(B, Tn, V, seed, lengths=False):
+    g = torch.Generator().manual_seed(seed)
+    logits = torch.randn(B, Tn, V, generator=g).to(torch.bfloat16)
+    ref_logits = (logits.float() + 0.1 * torch.randn(B, Tn, V, generator=g)).to(torch.bfloat16)
+    new_logits = (logits.float() + 0.05 * torch.randn(B, Tn, V, generator=g)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, Tn), generator=g)
+    old_values = torch.randn(B, Tn, generator=g)
+    values = old_values + 0.3 * torch.randn(B, Tn, generator=g)
+    scores = torch.rand(B, generator=g) * 24 - 12
+    L = mask = None
+    if lengths:
+        L = torch.randint(1, Tn + 1, (B,), generator=g)
+        L[0] = Tn
+        mask = (torch.arange(Tn)[None, :] < L[:, None]).long()
+        old_values = old_values.masked_fill(mask == 0, 0)
+    return logits, ref_logits, new_logits, labels, old_values, values, scores, L, mask
+
+
+@pytest.mark.parametrize("B,Tn,V,lengths", [(4, 9, 1031, False), (8, 48, 50257, False), (16, 48, 32128, True),
+                                            (128, 48, 50257, False)])
+def test_hot_path_step_vs_oracle(B, Tn, V, lengths):
+    """PPOHotPath.step (K1..K6) vs the oracle's restated step; the last case is the full
+    GPT-2 sentiments bench shape (configs[1])."""
+    logits, ref_logits, new_logits, labels, old_values, values, scores, L, mask = _step_inputs(B, Tn, V, B + V,
+                                                                                               lengths)
+    hp = P.PPOHotPath(P.PPOConfig(), B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05)
+    loss, stats, dlogits, dvalues = hp.step(cuda(logits), cuda(ref_logits), cuda(new_logits), cuda(labels),
+                                            cuda(old_values), cuda(values), cuda(scores),
+                                            lengths=None if L is None else cuda(L),
+                                            mask=None if mask is None else cuda(mask))
+    torch.cuda.synchronize()
+    ref = orc.ppo_step_reference(logits.float(), ref_logits.float(), new_logits.float(), labels, old_values,
+                                 values, scores, kl_coef=0.05, lengths=L, mask=mask)
+    torch.testing.assert_close(hp.lp_old.cpu(), ref["lp"], **RT32)
+    torch.testing.assert_close(hp.ref_lp.cpu(), ref["ref_lp"], **RT32)
+    torch.testing.assert_close(hp.rewards.cpu(), ref["rewards"], **RT32)
+    torch.testing.assert_close(hp.returns.cpu(), ref["returns"], **RT32)
+    torch.testing.assert_close(hp.lp_new.cpu(), ref["new_lp"], **RT32)
+    torch.testing.assert_close(loss.cpu().reshape(()), ref["loss"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dvalues.cpu(), ref["dvalues"], rtol=1e-5, atol=1e-9)
+    # dlogits are written in the logits dtype (bf16): one rounding of the fp32 value
+    torch.testing.assert_close(dlogits.float().cpu(), ref["dlogits"], rtol=8e-3, atol=1e-9)
+    st = stats.cpu().tolist()
+    for i, k in enumerate(P.STATS_KEYS):
+        assert st[i] == pytest.approx(float(ref["stats"][k]), rel=1e-5, abs=1e-6), k
+    # size-independent properties at full size: every dlogits row sums to ~0
+    row_sum = dlogits.float().sum(-1)
+    assert row_sum.abs().max().item() < 1e-3
+
+
+def test_hot_path_step_is_deterministic():
+    args = _step_inputs(32, 48, 50257, 11)
+    logits, ref_logits, new_logits, labels, old_values, values, scores, _, _ = args
+    d = [cuda(t) for t in (logits, ref_logits, new_logits, labels, old_values, values, scores)]
+    outs = []
+    for _ in range(2):
+        hp = P.PPOHotPath(P.PPOConfig(), 32, 48, 50257, torch.bfloat16, DEV, kl_coef=0.05)
+        loss, stats, dl, dv = hp.step(*d)
+        outs.append((loss.clone(), stats.clone(), dl.clone(), dv.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -1,0 +1,133 @@
+"""CPU-only checks of the host side: the C-ABI library's exported symbols, the ctypes
+signature table, host scalar logic (KL controllers, RunningMoments merge, flatten_dict,
+stats layout), grad-buffer phase logic, and the gloo (world 2) DP statistics exchange."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import trlx_t5_amd as P
+from trlx_t5_amd import _lib
+from trlx_t5_amd.modeling import _allreduce_moments, merge_moments, moments_to_mean_var
+from golden_util import T
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "trlx_t5_amd.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(trlx_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_the_binding_table():
+    assert set(header_functions()) == set(_lib.SIGNATURES)
+
+
+@pytest.fixture(scope="module")
+def built_lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "trlx-t5_amd", "csrc"), "-j8"])
+    return _lib.load()
+
+
+def test_library_exports_every_declared_symbol(built_lib):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH]).decode()
+    exported = set(re.findall(r"\bT (trlx_\w+)", out))
+    missing = set(header_functions()) - exported
+    assert not missing, f"declared but not exported: {missing}"
+    assert built_lib.trlx_abi_version() == _lib.ABI_VERSION
+
+
+def test_library_is_gfx950_code(built_lib):
+    assert b"gfx950" in open(_lib.LIB_PATH, "rb").read()
+
+
+def test_kernels_refuse_cpu_tensors():
+    x = torch.randn(2, 3, 11)
+    y = torch.zeros(2, 3, dtype=torch.long)
+    with pytest.raises(ValueError, match="ROCm"):
+        P.logprobs_from_logits(x, y)
+    with pytest.raises(ValueError):
+        P.whiten(torch.randn(4, 4))
+
+
+def test_kl_controllers(golden):
+    z = golden("host_state")
+    kl = P.AdaptiveKLController(0.05, 6, 10000)
+    for c, want in zip(z["kl/currents"], z["kl/values"]):
+        kl.update(float(c), n_steps=12)
+        assert kl.value == pytest.approx(float(want), rel=1e-15)
+    fk = P.FixedKLController(0.05)
+    fk.update(3.0, 12)
+    assert fk.value == float(z["kl/fixed"])
+
+
+def test_running_moments_merge_kat(golden):
+    """The reference KAT (tests/test_ppo.py:49-66) through the host merge the device path uses."""
+    z = golden("host_state")
+    mean, var, count = 0.0, 1.0, 1e-24
+    for i in range(4):
+        a = np.asarray(z[f"rm/{i}/in"], dtype=np.float64)
+        n = a.size
+        xm, xv = a.mean(), a.var()
+        mean, var, std, count = merge_moments(mean, var, count, xm, xv, n)
+        assert mean == pytest.approx(float(z[f"rm/{i}/mean"]), rel=1e-12)
+        assert std == pytest.approx(float(z[f"rm/{i}/std"]), rel=1e-12)
+        assert (xv * n / (n - 1)) ** 0.5 == pytest.approx(float(z[f"rm/{i}/batch_std"]), rel=1e-12)
+    allv = np.concatenate([np.asarray(z[f"rm/{i}/in"]) for i in range(4)])
+    assert mean == pytest.approx(allv.mean(), abs=1e-6)
+    assert std == pytest.approx(allv.std(ddof=1), abs=1e-6)
+
+
+def test_flatten_dict_and_stats_layout():
+    d = {"losses": {"a": 1, "b": {"c": 2}}, "ratio": 3}
+    assert P.flatten_dict(d) == {"losses/a": 1, "losses/b/c": 2, "ratio": 3}
+    assert len(P.STATS_KEYS) == _lib.PPO_STATS
+    from oracle import ppo_oracle as orc
+    n = 6
+    _, stats = orc.ppo_loss(torch.zeros(2, 3), torch.zeros(2, 3), torch.zeros(2, 3), torch.zeros(2, 3),
+                            torch.zeros(2, 3), torch.ones(2, 3), torch.ones(2, 3, dtype=torch.long))
+    assert set(stats) == set(P.STATS_KEYS)
+    del n
+
+
+@pytest.mark.parametrize("shape_stride", [((3, 5, 37), None), ((4, 6, 11), "slice")])
+def test_grad_buffer_phase(shape_stride):
+    shape, kind = shape_stride
+    full = torch.randn(shape[0] + 1, *shape[1:], dtype=torch.bfloat16)
+    x = full[:, :-1] if kind else full[:-1]
+    for off in range(4):
+        xv = full.view(-1)[off:off + x.numel()].view(x.shape) if kind is None else x
+        d = P.grad_buffer_like(xv)
+        assert d.shape == xv.shape and d.stride() == xv.stride()
+        assert (d.data_ptr() - xv.data_ptr()) % 16 == 0
+
+
+@pytest.mark.parametrize("world", [2])
+def test_dp_whitening_statistics_gloo(golden, world):
+    """world-2 gloo: the one-shot {sum, sumsq, n} all-reduce reproduces the reference's
+    two-phase global mean / biased variance (modeling.py:9-21, fixture from gloo ranks)."""
+    import torch.multiprocessing as mp
+    z = golden("whiten")
+    xs = T(z["f32_big/xs"])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 200
+    import dist_workers
+    ps = [ctx.Process(target=dist_workers.whiten_stats_worker, args=(r, world, port, xs, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    for _, mean, var, cnt in res:
+        assert mean == pytest.approx(float(z[f"f32_big/dist{world}/mean"]), rel=1e-6)
+        assert var == pytest.approx(float(z[f"f32_big/dist{world}/var"]), rel=1e-6)
+        assert cnt == float(z[f"f32_big/dist{world}/count"])
+        w = (xs - mean) * torch.rsqrt(torch.tensor(var, dtype=torch.float32) + 1e-8)
+        torch.testing.assert_close(w, T(z[f"f32_big/dist{world}/whiten"]), rtol=1e-5, atol=1e-5)

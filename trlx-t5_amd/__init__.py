@@ -1,0 +1,32 @@
+"""trlx_t5_amd — MI355X-native (gfx950) PPO experience-and-loss hot path of trlX-T5.
+
+Drop-in names (reference file:line in danyang-rainbow/trlx-t5):
+  logprobs_from_logits, whiten, get_global_statistics, RunningMoments, flatten_dict
+      trlx/utils/modeling.py
+  PPOConfig (.get_advantages_and_returns, .loss, .loss_from_logits),
+  AdaptiveKLController, FixedKLController
+      trlx/model/nn/ppo_models.py
+  kl_penalty_rewards, prepare_scores
+      trlx/orchestrator/ppo_orchestrator.py:96-112,163-167
+  PPOHotPath — the fused device-resident experience+loss step (bench / DP shard)
+
+All tensor math runs in hand-written HIP kernels (libtrlx_t5_amd.so, C ABI in
+include/trlx_t5_amd.h).  There is no CPU fallback.
+"""
+from . import _lib
+from .modeling import (RunningMoments, flatten_dict, get_global_statistics, grad_buffer_like,
+                       logprobs_from_logits, moments, whiten)
+from .ppo import (STATS_KEYS, AdaptiveKLController, FixedKLController, PPOConfig, kl_penalty_rewards,
+                  prepare_scores, stats_dict)
+from .step import PPOHotPath
+
+__all__ = [
+    "logprobs_from_logits", "whiten", "get_global_statistics", "RunningMoments", "flatten_dict", "moments",
+    "grad_buffer_like", "PPOConfig", "AdaptiveKLController", "FixedKLController", "kl_penalty_rewards",
+    "prepare_scores", "stats_dict", "STATS_KEYS", "PPOHotPath", "load_library",
+]
+
+
+def load_library():
+    """Load libtrlx_t5_amd.so now (raises if it is not built)."""
+    return _lib.load()

@@ -1,0 +1,119 @@
+"""ctypes binding of the C ABI in include/trlx_t5_amd.h (libtrlx_t5_amd.so, built in-tree
+for gfx950 by `make -C trlx-t5_amd/csrc` / `__graft_entry__.build()`).
+
+There is no fallback: if the shared library is missing or fails to load, every entry
+point raises.  torch is imported first so the HIP runtime the library links against
+(libamdhip64.so.7) resolves to the one torch already loaded — the library then launches
+on torch's streams directly.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtrlx_t5_amd.so")
+
+F32, BF16, I64 = 0, 1, 2
+ABI_VERSION = 1
+MOMENT_SLOTS = 4
+PPO_STATS = 13
+PPO_PARTIAL_SLOTS = 16
+
+_c_vp, _c_i64, _c_int, _c_f, _c_d = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double
+
+# name -> (restype, argtypes)   (must match include/trlx_t5_amd.h exactly)
+SIGNATURES = {
+    "trlx_abi_version": (_c_int, []),
+    "trlx_last_error": (ctypes.c_char_p, []),
+    "trlx_lsm_gather_fwd": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
+                                     _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
+    "trlx_lsm_gather_bwd": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
+                                     _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_i64, _c_i64, _c_vp]),
+    "trlx_kl_penalty_rewards": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_f, _c_vp, _c_vp,
+                                         _c_vp, _c_int, _c_vp]),
+    "trlx_gae_num_blocks": (_c_i64, [_c_i64, _c_i64]),
+    "trlx_gae_scan": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_vp, _c_vp,
+                               _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp,
+                               _c_vp]),
+    "trlx_moments_num_blocks": (_c_i64, [_c_i64]),
+    "trlx_moments_partial": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
+    "trlx_moments_finalize": (_c_int, [_c_vp, _c_i64, _c_vp, _c_vp]),
+    "trlx_whiten_apply": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp]),
+    "trlx_ppo_policy_fused": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
+                                       _c_i64, _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                       _c_d, _c_f, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp]),
+    "trlx_ppo_loss_num_blocks": (_c_i64, [_c_i64]),
+    "trlx_ppo_loss_elem": (_c_int, [_c_i64, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int,
+                                    _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_d,
+                                    _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_int, _c_vp, _c_vp]),
+    "trlx_ppo_loss_finalize": (_c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_d, _c_f, _c_vp, _c_vp, _c_vp]),
+    "trlx_scale_by": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
+}
+
+_lib = None
+
+
+class TrlxError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes handle; raises if the HIP library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise TrlxError(
+            f"{LIB_PATH} not found: the HIP extension is not built (run `python -c 'import "
+            f"__graft_entry__ as g; g.build()'` or `make -C trlx-t5_amd/csrc`). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.trlx_abi_version() != ABI_VERSION:
+        raise TrlxError(f"ABI mismatch: library {lib.trlx_abi_version()} vs binding {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke a status-returning entry point; raise on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.trlx_last_error().decode(errors="replace")
+        err = ValueError if rc in (1, 2, 3, 5) else TrlxError
+        raise err(f"{name} failed (status {rc}): {msg}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+# ------------------------------------------------------------------ tensor helpers
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.int64:
+        return I64
+    raise TypeError(f"unsupported dtype {t.dtype} (trlx_t5_amd kernels take float32 / bfloat16 / int64)")
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t):
+    """hipStream_t (as int) of torch's current stream on t's device."""
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("trlx_t5_amd: tensors must live on a ROCm (cuda) device; there is no CPU path")

@@ -1,0 +1,204 @@
+// Shared device helpers for the trlx_t5_amd HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "trlx_t5_amd.h"
+
+namespace trlx {
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kMaxThreads = 1024;  // largest workgroup we launch
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t vec4u __attribute__((ext_vector_type(4)));  // one 16-byte row vector
+__device__ __forceinline__ vec4u vec4u_make(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    vec4u r = {a, b, c, d};
+    return r;
+}
+
+// ------------------------------------------------------------------ bf16 <-> f32
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+// round-to-nearest-even, NaN preserving (lowers to v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+    bf16x2_t r;
+    r.x = (__bf16)a;
+    r.y = (__bf16)b;
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint16_t f2bf(float a) {
+    __bf16 h = (__bf16)a;
+    return __builtin_bit_cast(uint16_t, h);
+}
+
+// scalar load / store of a [n] vector of either dtype
+__device__ __forceinline__ float ld_any(const void* p, int dtype, int64_t i) {
+    return dtype == TRLX_BF16 ? bf2f(reinterpret_cast<const uint16_t*>(p)[i])
+                              : reinterpret_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void st_any(void* p, int dtype, int64_t i, float v) {
+    if (dtype == TRLX_BF16)
+        reinterpret_cast<uint16_t*>(p)[i] = f2bf(v);
+    else
+        reinterpret_cast<float*>(p)[i] = v;
+}
+
+// ------------------------------------------------------------------ fast transcendentals
+// v_exp_f32 computes 2^x; callers pre-scale by log2(e) (folded into an fma).
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// IEEE ops that must not be contracted into fma (the reference evaluates them as
+// separately rounded torch ops).
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+
+// ------------------------------------------------------------------ wave / block reductions
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+// Block reductions over blockDim.x (multiple of 64, <= 1024) threads.  `sh` must hold
+// blockDim.x/64 slots and be private to this call site (no trailing barrier: every
+// thread reads all slots after the one barrier, so a later reduction must use its own
+// slots).  The cross-wave order is fixed => deterministic.
+__device__ __forceinline__ float block_max(float v, float* sh) {
+    v = wave_max(v);
+    const int nw = blockDim.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) sh[threadIdx.x / kWave] = v;
+    __syncthreads();
+    float r = sh[0];
+    for (int i = 1; i < nw; ++i) r = fmaxf(r, sh[i]);
+    return r;
+}
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+    v = wave_sum(v);
+    const int nw = blockDim.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) sh[threadIdx.x / kWave] = v;
+    __syncthreads();
+    float r = sh[0];
+    for (int i = 1; i < nw; ++i) r += sh[i];
+    return r;
+}
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+    v = wave_sum_d(v);
+    const int nw = blockDim.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) sh[threadIdx.x / kWave] = v;
+    __syncthreads();
+    double r = sh[0];
+    for (int i = 1; i < nw; ++i) r += sh[i];
+    return r;
+}
+
+// ------------------------------------------------------------------ 16-byte row vectors
+// A logits row is split into [head | 16-B aligned body | tail]; head/tail have < EPV
+// elements.  Traits per storage type:
+struct F32T {
+    static constexpr int kEPV = 4;        // elements per 16-B vector
+    static constexpr uint32_t kNegInf = 0xff800000u;
+    typedef float elem_t;
+    __device__ static __forceinline__ float get(const vec4u& v, int e) {
+        const uint32_t w = e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+        return __uint_as_float(w);
+    }
+    __device__ static __forceinline__ void unpack(const vec4u& v, float (&f)[kEPV]) {
+        f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+        f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+    }
+    __device__ static __forceinline__ vec4u pack(const float (&f)[kEPV]) {
+        return vec4u_make(__float_as_uint(f[0]), __float_as_uint(f[1]),
+                          __float_as_uint(f[2]), __float_as_uint(f[3]));
+    }
+    __device__ static __forceinline__ vec4u neg_inf() {
+        return vec4u_make(kNegInf, kNegInf, kNegInf, kNegInf);
+    }
+    __device__ static __forceinline__ float load1(const void* row, int64_t j) {
+        return reinterpret_cast<const float*>(row)[j];
+    }
+    __device__ static __forceinline__ void store1(void* row, int64_t j, float v) {
+        reinterpret_cast<float*>(row)[j] = v;
+    }
+};
+struct BF16T {
+    static constexpr int kEPV = 8;
+    static constexpr uint32_t kNegInf2 = 0xff80ff80u;
+    typedef uint16_t elem_t;
+    __device__ static __forceinline__ void unpack(const vec4u& v, float (&f)[kEPV]) {
+        f[0] = bf_lo(v.x); f[1] = bf_hi(v.x); f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+        f[4] = bf_lo(v.z); f[5] = bf_hi(v.z); f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
+    }
+    __device__ static __forceinline__ vec4u pack(const float (&f)[kEPV]) {
+        return vec4u_make(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]),
+                          pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+    }
+    __device__ static __forceinline__ vec4u neg_inf() {
+        return vec4u_make(kNegInf2, kNegInf2, kNegInf2, kNegInf2);
+    }
+    __device__ static __forceinline__ float load1(const void* row, int64_t j) {
+        return bf2f(reinterpret_cast<const uint16_t*>(row)[j]);
+    }
+    __device__ static __forceinline__ void store1(void* row, int64_t j, float v) {
+        reinterpret_cast<uint16_t*>(row)[j] = f2bf(v);
+    }
+};
+
+// Geometry of one row: element pointer p (naturally aligned), V elements.
+template <class DT>
+struct RowSplit {
+    int head;       // elements before the first 16-B boundary (< EPV)
+    int64_t nvec;   // full 16-B vectors in the body
+    int64_t tail0;  // first tail element
+    int tail;       // tail elements (< EPV)
+    __device__ __forceinline__ RowSplit(const void* p, int64_t V) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        int h = int(((16u - (a & 15u)) & 15u) / sizeof(typename DT::elem_t));
+        if (h > V) h = int(V);
+        head = h;
+        nvec = (V - h) / DT::kEPV;
+        tail0 = h + nvec * DT::kEPV;
+        tail = int(V - tail0);
+    }
+};
+
+// Opaque register copy: stops the compiler from keeping the unpacked fp32 copy of a
+// register-resident bf16 row alive across the max / sum / store passes (it would double
+// the row's VGPR footprint); unpacking again is 1-2 VALU ops per pair.
+__device__ __forceinline__ void launder(vec4u& v) { asm volatile("" : "+v"(v)); }
+
+// Streaming (read-once) 16-B load.
+__device__ __forceinline__ vec4u ld_stream(const vec4u* p) {
+    return __builtin_nontemporal_load(p);
+}
+
+}  // namespace trlx
+
+// ------------------------------------------------------------------ host-side error plumbing
+namespace trlx {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace trlx
+
+#define TRLX_REQUIRE(cond, code, ...)          \
+    do {                                       \
+        if (!(cond)) {                         \
+            ::trlx::set_error(__VA_ARGS__);    \
+            return (code);                     \
+        }                                      \
+    } while (0)

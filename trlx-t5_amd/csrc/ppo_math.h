@@ -1,0 +1,52 @@
+// Per-token PPO arithmetic shared by the fused vocab-row kernel and the [B,T] loss kernel.
+#pragma once
+#include "common.h"
+
+namespace trlx {
+
+// Closed-form d(policy loss)/d(logprob) for one token, following the autograd graph of
+// ppo_models.py:165-177:  lr = (lp-olp)*m;  ratio = exp(lr);
+//   pg = max(-A*ratio, -A*clamp(ratio, 1-c, 1+c));  loss_pg = sum(pg*m) / sum(m)
+// torch.maximum splits the gradient 1/2-1/2 on ties; clamp passes it on its inclusive
+// bounds.  Also returns the forward terms the stats need.
+struct PolicyTerms {
+    float ratio, lr, pgmax;
+    bool pgclip;
+};
+__device__ __forceinline__ float ppo_policy_dlp(float lp, float olp, float A, float m, float inv_msum,
+                                                float c, PolicyTerms& o) {
+    o.lr = mul_rn(lp - olp, m);
+    o.ratio = expf(o.lr);
+    const float negA = -A;
+    const float lo = 1.0f - c, hi = 1.0f + c;
+    const float pg1 = mul_rn(negA, o.ratio);
+    const float cr = fminf(fmaxf(o.ratio, lo), hi);
+    const float pg2 = mul_rn(negA, cr);
+    o.pgmax = fmaxf(pg1, pg2);
+    o.pgclip = pg2 > pg1;
+    const float u = mul_rn(inv_msum, m);
+    float g1, g2;
+    if (pg1 == pg2) {
+        g1 = u * 0.5f;
+        g2 = g1;
+    } else {
+        g1 = pg1 > pg2 ? u : 0.0f;
+        g2 = pg1 > pg2 ? 0.0f : u;
+    }
+    const float inr = (o.ratio >= lo && o.ratio <= hi) ? 1.0f : 0.0f;
+    const float dratio = add_rn(mul_rn(g1, negA), mul_rn(mul_rn(g2, negA), inr));
+    return mul_rn(mul_rn(dratio, o.ratio), m);
+}
+
+// mean and rsqrt(var + 1e-8) from a {sum, sumsq, count} fp64 record (modeling.py:24-34):
+// var = M2/count in the distributed branch, M2/(count-1) for torch.var_mean.
+__device__ __forceinline__ void whiten_coeffs(const double* st, int unbiased, float& mu, float& rstd) {
+    const double cnt = st[2];
+    const double mean = st[0] / cnt;
+    double m2 = st[1] - st[0] * mean;
+    if (m2 < 0) m2 = 0;
+    mu = float(mean);
+    rstd = rsqrtf(float(m2 / (unbiased ? cnt - 1.0 : cnt)) + 1e-8f);
+}
+
+}  // namespace trlx

@@ -1,0 +1,212 @@
+"""Drop-in for trlx/utils/modeling.py (reference file) on MI355X.
+
+Same names, signatures and return conventions as the reference; every tensor
+computation is a HIP kernel from libtrlx_t5_amd.so (no CPU path):
+
+  get_global_statistics  modeling.py:9-21   partial moments + RCCL all-reduce of {sum, sumsq, n}
+  whiten                 modeling.py:24-34  biased (distributed branch) / unbiased (var_mean)
+  logprobs_from_logits   modeling.py:37-41  fused single-pass log-softmax + gather, autograd
+  flatten_dict           modeling.py:44-57  host utility
+  RunningMoments         modeling.py:72-104 Chan merge of batch moments (host scalars)
+"""
+from collections.abc import MutableMapping
+from typing import Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+__all__ = ["get_global_statistics", "whiten", "logprobs_from_logits", "flatten_dict", "RunningMoments",
+           "moments", "grad_buffer_like"]
+
+
+# ------------------------------------------------------------------ moments (A3)
+def moments(xs: torch.Tensor) -> torch.Tensor:
+    """fp64 [4] device tensor {sum, sum of squares, count, 0} of xs (deterministic)."""
+    _lib.require_cuda(xs)
+    x = xs.contiguous()
+    n = x.numel()
+    nblk = _lib.query("trlx_moments_num_blocks", n)
+    part = torch.empty(nblk * _lib.MOMENT_SLOTS, dtype=torch.float64, device=x.device)
+    st = torch.empty(_lib.MOMENT_SLOTS, dtype=torch.float64, device=x.device)
+    s = _lib.stream_of(x)
+    _lib.call("trlx_moments_partial", _lib.ptr(x), _lib.dtype_code(x), n, _lib.ptr(part), s)
+    _lib.call("trlx_moments_finalize", _lib.ptr(part), nblk, _lib.ptr(st), s)
+    return st
+
+
+def _allreduce_moments(st: torch.Tensor) -> torch.Tensor:
+    """SUM {sum, sumsq, count} across ranks (one fp64 RCCL all-reduce, modeling.py:14,19)."""
+    if dist.is_available() and dist.is_initialized():
+        head = st[:3]
+        dist.all_reduce(head, dist.ReduceOp.SUM)
+    return st
+
+
+def moments_to_mean_var(st: torch.Tensor, unbiased: bool):
+    """{sum, sumsq, count} -> (mean, var) as fp64 0-d tensors on st's device (no sync).
+    Same formula the kernels use (ppo_math.h whiten_coeffs)."""
+    total, sumsq, count = st[0], st[1], st[2]
+    mean = total / count
+    m2 = (sumsq - total * mean).clamp_min(0)
+    return mean, m2 / ((count - 1) if unbiased else count)
+
+
+def get_global_statistics(xs: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Global mean and biased variance of xs across processes (modeling.py:9-21).
+
+    Returns 0-d tensors in xs.dtype like the reference (which builds its all-reduce
+    buffer in xs.dtype).  The accumulation itself is fp64 on device and one all-reduce.
+    """
+    st = _allreduce_moments(moments(xs))
+    mean, var = moments_to_mean_var(st, unbiased=False)
+    return mean.to(xs.dtype), var.to(xs.dtype), st[2].to(xs.dtype)
+
+
+def whiten(xs: torch.Tensor, shift_mean=True, distributed=True) -> torch.Tensor:
+    """(xs - mean) * rsqrt(var + 1e-8) (+ mean if not shift_mean)  — modeling.py:24-34.
+
+    distributed and torch.distributed initialised -> global biased variance (one
+    all-reduce); otherwise torch.var_mean semantics (unbiased).
+    """
+    use_dist = distributed and dist.is_available() and dist.is_initialized()
+    st = moments(xs)
+    if use_dist:
+        _allreduce_moments(st)
+    x = xs.contiguous()
+    out = torch.empty_like(x)
+    _lib.call("trlx_whiten_apply", _lib.ptr(x), _lib.dtype_code(x), x.numel(), _lib.ptr(st),
+              0 if use_dist else 1, 1 if shift_mean else 0, _lib.ptr(out), _lib.dtype_code(out),
+              _lib.stream_of(x))
+    return out.view_as(xs)
+
+
+# ------------------------------------------------------------------ logprobs (A1)
+def _token_geometry(logits: torch.Tensor, labels: torch.Tensor):
+    """Express logits[..., V] / labels[...] as (B, T, V, sb, st) / (lb, lt) strided views."""
+    if logits.dim() < 2:
+        raise ValueError("logits must have at least 2 dims [..., V]")
+    if tuple(labels.shape) != tuple(logits.shape[:-1]):
+        raise ValueError(f"labels shape {tuple(labels.shape)} must equal logits.shape[:-1] {tuple(logits.shape[:-1])}")
+    if labels.dtype != torch.int64:
+        raise TypeError("labels must be int64 (torch.gather index)")
+    if logits.stride(-1) != 1:
+        logits = logits.contiguous()
+    if logits.dim() == 2:
+        N, V = logits.shape
+        return logits, labels, (N, 1, V, logits.stride(0), 0), (labels.stride(0), 0)
+    if logits.dim() > 3:
+        lead = logits.shape[:-2]
+        logits = logits.reshape(-1, logits.shape[-2], logits.shape[-1])
+        labels = labels.reshape(-1, labels.shape[-1])
+        del lead
+    B, T, V = logits.shape
+    return logits, labels, (B, T, V, logits.stride(0), logits.stride(1)), (labels.stride(0), labels.stride(1))
+
+
+def grad_buffer_like(x: torch.Tensor) -> torch.Tensor:
+    """Uninitialised tensor with x's size/strides whose rows have x's 16-byte phase, so the
+    kernels can write dlogits with the same aligned 16-B vectors they read logits with."""
+    es = x.element_size()
+    extent = 1 + sum((s - 1) * st for s, st in zip(x.shape, x.stride()) if s > 0)
+    pad = 16 // es
+    buf = torch.empty(extent + pad, dtype=x.dtype, device=x.device)
+    off = ((x.data_ptr() - buf.data_ptr()) % 16) // es
+    return buf.as_strided(x.shape, x.stride(), off)
+
+
+class _LogprobsFromLogits(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        _lib.require_cuda(logits, labels)
+        orig_shape = labels.shape
+        lg, lb, (B, T, V, sb, st), (l0, l1) = _token_geometry(logits, labels)
+        out = torch.empty((B, T), dtype=logits.dtype, device=logits.device)
+        lse = torch.empty((B, T), dtype=torch.float32, device=logits.device)
+        _lib.call("trlx_lsm_gather_fwd", _lib.ptr(lg), None, _lib.dtype_code(lg), B, T, V, sb, st,
+                  _lib.ptr(lb), l0, l1, _lib.ptr(out), None, _lib.dtype_code(out), _lib.ptr(lse), None,
+                  _lib.stream_of(lg))
+        ctx.save_for_backward(lg, lb, lse)
+        ctx.geom = (B, T, V, sb, st, l0, l1)
+        ctx.logits_meta = (logits.shape, lg is logits)
+        return out.view(orig_shape)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        lg, lb, lse = ctx.saved_tensors
+        B, T, V, sb, st, l0, l1 = ctx.geom
+        g = grad_out.contiguous()
+        if g.dtype not in (torch.float32, torch.bfloat16):
+            g = g.float()
+        dx = grad_buffer_like(lg)
+        dsb, dst = (dx.stride(0), dx.stride(1)) if dx.dim() == 3 else (dx.stride(0), 0)
+        _lib.call("trlx_lsm_gather_bwd", _lib.ptr(lg), _lib.dtype_code(lg), B, T, V, sb, st, _lib.ptr(lb),
+                  l0, l1, _lib.ptr(lse), _lib.ptr(g), _lib.dtype_code(g), _lib.ptr(dx), dsb, dst,
+                  _lib.stream_of(lg))
+        shape, same = ctx.logits_meta
+        return (dx if same else dx.reshape(shape)), None
+
+
+def logprobs_from_logits(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """log_softmax(logits, -1).gather(-1, labels[..., None]).squeeze(-1) — modeling.py:37-41.
+
+    One HBM pass over each vocab row (the [.., V] log-softmax is never materialised);
+    differentiable w.r.t. logits (backward = one read + one write of the row).  Output dtype
+    = logits dtype, like the reference.
+    """
+    return _LogprobsFromLogits.apply(logits, labels)
+
+
+# ------------------------------------------------------------------ host utilities
+def flatten_dict(d, parent_key: str = "", sep: str = "/") -> dict:
+    """Nested dict -> flat dict with `sep`-joined keys (modeling.py:44-57)."""
+    items = {}
+    for k, v in d.items():
+        key = f"{parent_key}{sep}{k}" if parent_key else k
+        if isinstance(v, MutableMapping):
+            items.update(flatten_dict(v, key, sep=sep))
+        else:
+            items[key] = v
+    return items
+
+
+def merge_moments(mean, var, count, xs_mean, xs_var, xs_count):
+    """Chan/parallel merge used by RunningMoments.update (modeling.py:91-102); host floats.
+
+    Returns (new_mean, new_var, new_std(unbiased), new_count)."""
+    delta = xs_mean - mean
+    tot = count + xs_count
+    new_sum = xs_var * xs_count
+    old_sum = var * count + delta ** 2 * count * xs_count / tot
+    new_mean = mean + delta * xs_count / tot
+    new_var = (old_sum + new_sum) / tot
+    new_std = (new_var * tot / (tot - 1)) ** 0.5
+    return new_mean, new_var, new_std, tot
+
+
+class RunningMoments:
+    """Running mean / std of a scalar stream (modeling.py:72-104).
+
+    Batch moments come from the device moments kernel (all-reduced across ranks when
+    torch.distributed is initialised); the merge itself is host fp64 scalar arithmetic.
+    """
+
+    def __init__(self):
+        self.mean = 0.0
+        self.std = 1.0
+        self.var = 1.0
+        self.count = 1e-24
+
+    def update(self, xs: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        st = moments(xs)
+        if dist.is_available() and dist.is_initialized():
+            _allreduce_moments(st)
+        s, ss, n = st[:3].tolist()
+        xs_mean = s / n
+        xs_var = max(ss - s * xs_mean, 0.0) / n  # biased, as var_mean(unbiased=False)
+        self.mean, self.var, self.std, self.count = merge_moments(
+            float(self.mean), float(self.var), float(self.count), xs_mean, xs_var, n)
+        batch_std = (xs_var * n / (n - 1)) ** 0.5 if n > 1 else float("nan")
+        return (torch.tensor(xs_mean, dtype=torch.float64),
+                torch.tensor(batch_std, dtype=torch.float64))
