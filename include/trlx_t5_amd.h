@@ -58,6 +58,14 @@ typedef enum {
 int trlx_abi_version(void);
 const char* trlx_last_error(void);
 
+/* Process-wide launch tuning (0 = automatic, the default).  Keys:
+ *   "row_variant"       1 = register-resident vocab rows, 2 = streaming vocab rows
+ *   "resident_threads"  workgroup size for resident rows (multiple of 64)
+ *   "stream_threads"    workgroup size for streaming rows
+ *   "stream_unroll"     16-B loads in flight per thread for streaming rows (2, 4, 8)
+ * Results are identical up to fp32 summation order; only speed changes. */
+int trlx_set_tuning(const char* key, int64_t value);
+
 /* ---------------------------------------------------------------- A1
  * logprobs_from_logits forward — replaces trlx/utils/modeling.py:37-41
  * (F.log_softmax over V + gather at labels), fused in one pass over each row; the
@@ -103,14 +111,17 @@ int trlx_kl_penalty_rewards(const void* lp, const void* ref_lp, int in_dtype,
  * Outputs: adv_raw fp32 [B,Teff] (unwhitened), ret [B,Teff] of ret_dtype, and per-block
  * partial moments of adv_raw: partials[blk*4 + {0,1,2,3}] = {sum A, sum A^2, count,
  * sum mask} (mask: int64 [B,Teff] loss mask, NULL = all ones).
- * trlx_gae_num_blocks(B, Teff) tells how many partial records are written. */
+ * trlx_gae_num_blocks(B, Teff) tells how many partial records are written.  With
+ * stats != NULL the last block to finish also reduces them (fixed order) into stats[4];
+ * `ticket` is then a device uint32 that must be 0 before the first call (the kernel
+ * re-arms it). */
 int64_t trlx_gae_num_blocks(int64_t B, int64_t Teff);
 int trlx_gae_scan(const void* values, const void* rewards, int dtype, int64_t B, int64_t T,
                   int64_t Teff, float gamma, float lam,
                   const float* lp, const float* ref_lp, float neg_beta, const float* scores,
                   const int64_t* lengths, const int64_t* mask,
                   float* adv_raw, void* ret, int ret_dtype, void* rew_out, int rew_dtype,
-                  double* partials, void* stream);
+                  double* partials, double* stats, unsigned* ticket, void* stream);
 
 /* ---------------------------------------------------------------- A3 helpers
  * Partial moments of an arbitrary contiguous tensor (for whiten / get_global_statistics,
@@ -160,7 +171,10 @@ int trlx_ppo_loss_elem(int64_t n, const void* lp, int lp_dtype, const void* valu
                        const double* adv_stats, int unbiased, const void* returns,
                        int r_dtype, const int64_t* mask, const double* msum, double msum_host,
                        float cliprange, float cliprange_value, float vf_coef,
-                       void* dlp, void* dv, int g_dtype, double* partials, void* stream);
+                       void* dlp, void* dv, int g_dtype, double* partials,
+                       float* loss, float* stats, unsigned* ticket, void* stream);
+/* (with ticket != NULL — a device uint32, 0 before the first call — the last block of
+ *  trlx_ppo_loss_elem performs pass 2 itself: one launch for the whole loss.) */
 int trlx_ppo_loss_finalize(const double* partials, int64_t nblk, int64_t n,
                            const double* msum, double msum_host, float vf_coef,
                            float* loss, float* stats, void* stream);

@@ -1,0 +1,38 @@
+#!/bin/bash
+# Runs GPU steps on the gpurun box; each step has its own time limit and the script
+# stops at the first step that faults / aborts / times out (any rc other than 0 or 1).
+#   scripts/gpu_run.sh smoke tests bench profile pmc
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+    local name=$1 lim=$2; shift 2
+    local t0=$(date +%s)
+    timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc ($(( $(date +%s) - t0 ))s)"
+    tail -n 4 "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+        echo "stopping after $name (rc=$rc)"; exit $rc
+    fi
+}
+for step in "$@"; do
+    case $step in
+        smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        tests) run gpu_tests 1100 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+        testsall) run gpu_tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+        sweep) run sweep 300 python tools/row_sweep.py ;;
+        sweep_c4) B=128 T=128 V=32128 run sweep_c4 300 python tools/row_sweep.py ;;
+        bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;
+        bench_c3) run bench_c3 300 python bench.py --steps 20 --warmup 5 --config c3 --cpu-seconds 0 ;;
+        bench_c4) run bench_c4 300 python bench.py --steps 20 --warmup 5 --config c4 --cpu-seconds 0 ;;
+        profile) run profile 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
+                     -o run -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+        pmc_fetch) run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch \
+                     -o run -- python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-timers ;;
+        pmc_write) run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write \
+                     -o run -- python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-timers ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done

@@ -26,6 +26,7 @@ _c_vp, _c_i64, _c_int, _c_f, _c_d = ctypes.c_void_p, ctypes.c_int64, ctypes.c_in
 SIGNATURES = {
     "trlx_abi_version": (_c_int, []),
     "trlx_last_error": (ctypes.c_char_p, []),
+    "trlx_set_tuning": (_c_int, [ctypes.c_char_p, _c_i64]),
     "trlx_lsm_gather_fwd": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                      _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
     "trlx_lsm_gather_bwd": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
@@ -35,7 +36,7 @@ SIGNATURES = {
     "trlx_gae_num_blocks": (_c_i64, [_c_i64, _c_i64]),
     "trlx_gae_scan": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_f, _c_f, _c_vp, _c_vp,
                                _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp,
-                               _c_vp]),
+                               _c_vp, _c_vp, _c_vp]),
     "trlx_moments_num_blocks": (_c_i64, [_c_i64]),
     "trlx_moments_partial": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
     "trlx_moments_finalize": (_c_int, [_c_vp, _c_i64, _c_vp, _c_vp]),
@@ -46,7 +47,8 @@ SIGNATURES = {
     "trlx_ppo_loss_num_blocks": (_c_i64, [_c_i64]),
     "trlx_ppo_loss_elem": (_c_int, [_c_i64, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int,
                                     _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_d,
-                                    _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_int, _c_vp, _c_vp]),
+                                    _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                                    _c_vp]),
     "trlx_ppo_loss_finalize": (_c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_d, _c_f, _c_vp, _c_vp, _c_vp]),
     "trlx_scale_by": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
 }
@@ -87,6 +89,11 @@ def call(name, *args):
         err = ValueError if rc in (1, 2, 3, 5) else TrlxError
         raise err(f"{name} failed (status {rc}): {msg}")
     return rc
+
+
+def set_tuning(key: str, value: int):
+    """Launch-geometry knob (see trlx_set_tuning in include/trlx_t5_amd.h)."""
+    call("trlx_set_tuning", key.encode(), int(value))
 
 
 def query(name, *args):

@@ -107,6 +107,32 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
     return r;
 }
 
+// ------------------------------------------------------------------ last-block hand-off
+// Returns true (in every thread) in the one block of the grid that arrives last; all other
+// blocks' prior global stores are then visible to that block.  Protocol of
+// MI355X_MICROARCH.md "Valid forms" (producer: plain stores -> every wave vmcnt(0) ->
+// barrier -> lane-0 agent release fence -> asm vmcnt(0) -> agent atomic; consumer:
+// agent acquire fence -> vmcnt(0) -> barrier -> plain loads).  `ticket` must be 0 at
+// launch; the last block re-arms it to 0 for the next (stream-ordered) launch.
+__device__ __forceinline__ bool last_block_arrived(unsigned* ticket, unsigned nblocks) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (t == nblocks - 1);
+        if (s_last) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+
 // ------------------------------------------------------------------ 16-byte row vectors
 // A logits row is split into [head | 16-B aligned body | tail]; head/tail have < EPV
 // elements.  Traits per storage type:

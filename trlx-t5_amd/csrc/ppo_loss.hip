@@ -20,11 +20,43 @@ struct LossArgs {
     float c, cv, vf_coef;
     void* dlp; void* dv; int g_dtype;
     double* partials;
+    float* loss; float* stats; unsigned* ticket;  // optional fused finalize (last block)
 };
 
 constexpr int kLossThreads = 256;
-constexpr int kLossPerBlock = kLossThreads * 8;
+constexpr int kLossPerBlock = kLossThreads * 2;  // many short blocks: latency, not bandwidth, bound
 constexpr int kSlots = TRLX_PPO_PARTIAL_SLOTS;
+
+// One block: fixed-order sum of the partial records, then the loss and the 13 stats
+// (ppo_models.py:162-198; the divisions by N are torch.mean, var is unbiased).
+__device__ void ppo_loss_reduce(const double* partials, int nblk, int64_t n, double msum, float vf_coef,
+                                float* loss, float* stats) {
+    __shared__ double red[kSlots][kMaxThreads / kWave];
+    double acc[kSlots];
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x)
+        for (int k = 0; k < kSlots; ++k) acc[k] += partials[int64_t(i) * kSlots + k];
+    for (int k = 0; k < kSlots; ++k) acc[k] = block_sum_d(acc[k], red[k]);
+    if (threadIdx.x != 0) return;
+    const double N = double(n);
+    const double vf = 0.5 * acc[0] / msum;
+    const double pg = acc[3] / msum;
+    const double tot = pg + double(vf_coef) * vf;
+    loss[0] = float(tot);
+    stats[0] = float(tot);                                  // losses/total_loss
+    stats[1] = float(pg);                                   // losses/policy_loss
+    stats[2] = float(vf);                                   // losses/value_loss
+    stats[3] = float(acc[5] / N);                           // values/mean_old_values
+    stats[4] = float((acc[6] - acc[5] * acc[5] / N) / (N - 1.0));  // values/var_old_values
+    stats[5] = float(acc[7] / N);                           // values/mean_values
+    stats[6] = float(acc[8] / N);                           // values/values_error
+    stats[7] = float(acc[1] / N);                           // values/clipfrac
+    stats[8] = float(acc[2] / N);                           // policy/approx_kl
+    stats[9] = float(acc[4] / N);                           // policy/clipfrac
+    stats[10] = float(acc[9] / N);                          // returns/mean
+    stats[11] = float((acc[10] - acc[9] * acc[9] / N) / (N - 1.0));  // returns/var
+    stats[12] = float(acc[11] / msum);                      // ratio
+}
 
 __global__ __launch_bounds__(kLossThreads) void k_ppo_loss_elem(LossArgs a) {
     __shared__ double red[kSlots][kLossThreads / kWave];
@@ -95,37 +127,14 @@ __global__ __launch_bounds__(kLossThreads) void k_ppo_loss_elem(LossArgs a) {
 #pragma unroll
         for (int k = 0; k < kSlots; ++k) p[k] = acc[k];
     }
+    if (a.ticket && last_block_arrived(a.ticket, gridDim.x))
+        ppo_loss_reduce(a.partials, gridDim.x, a.n, msum, a.vf_coef, a.loss, a.stats);
 }
 
 __global__ __launch_bounds__(256) void k_ppo_loss_finalize(const double* partials, int64_t nblk, int64_t n,
                                                            const double* msum_p, double msum_host,
                                                            float vf_coef, float* loss, float* stats) {
-    __shared__ double red[kSlots][256 / kWave];
-    double acc[kSlots];
-    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
-    for (int64_t i = threadIdx.x; i < nblk; i += 256)
-        for (int k = 0; k < kSlots; ++k) acc[k] += partials[i * kSlots + k];
-    for (int k = 0; k < kSlots; ++k) acc[k] = block_sum_d(acc[k], red[k]);
-    if (threadIdx.x != 0) return;
-    const double msum = msum_p ? *msum_p : msum_host;
-    const double N = double(n);
-    const double vf = 0.5 * acc[0] / msum;
-    const double pg = acc[3] / msum;
-    const double tot = pg + double(vf_coef) * vf;
-    loss[0] = float(tot);
-    stats[0] = float(tot);                                  // losses/total_loss
-    stats[1] = float(pg);                                   // losses/policy_loss
-    stats[2] = float(vf);                                   // losses/value_loss
-    stats[3] = float(acc[5] / N);                           // values/mean_old_values
-    stats[4] = float((acc[6] - acc[5] * acc[5] / N) / (N - 1.0));  // values/var_old_values
-    stats[5] = float(acc[7] / N);                           // values/mean_values
-    stats[6] = float(acc[8] / N);                           // values/values_error
-    stats[7] = float(acc[1] / N);                           // values/clipfrac
-    stats[8] = float(acc[2] / N);                           // policy/approx_kl
-    stats[9] = float(acc[4] / N);                           // policy/clipfrac
-    stats[10] = float(acc[9] / N);                          // returns/mean
-    stats[11] = float((acc[10] - acc[9] * acc[9] / N) / (N - 1.0));  // returns/var
-    stats[12] = float(acc[11] / msum);                      // ratio
+    ppo_loss_reduce(partials, int(nblk), n, msum_p ? *msum_p : msum_host, vf_coef, loss, stats);
 }
 
 // ------------------------------------------------------------------ autograd scaling
@@ -153,7 +162,8 @@ extern "C" int trlx_ppo_loss_elem(int64_t n, const void* lp, int lp_dtype, const
                                   const double* adv_stats, int unbiased, const void* returns, int r_dtype,
                                   const int64_t* mask, const double* msum, double msum_host,
                                   float cliprange, float cliprange_value, float vf_coef, void* dlp,
-                                  void* dv, int g_dtype, double* partials, void* stream) {
+                                  void* dv, int g_dtype, double* partials, float* loss, float* stats,
+                                  unsigned* ticket, void* stream) {
     TRLX_REQUIRE(lp && values && old_lp && old_values && adv && returns && partials, TRLX_ERR_ARG,
                  "NULL input to ppo loss");
     TRLX_REQUIRE(msum || msum_host > 0, TRLX_ERR_ARG, "mask sum must be positive");
@@ -163,7 +173,8 @@ extern "C" int trlx_ppo_loss_elem(int64_t n, const void* lp, int lp_dtype, const
     a.ov = old_values; a.ov_dtype = ov_dtype; a.adv = adv; a.a_dtype = a_dtype; a.adv_stats = adv_stats; a.unbiased = unbiased;
     a.ret = returns; a.r_dtype = r_dtype; a.mask = mask; a.msum = msum; a.msum_host = msum_host;
     a.c = cliprange; a.cv = cliprange_value; a.vf_coef = vf_coef; a.dlp = dlp; a.dv = dv;
-    a.g_dtype = g_dtype; a.partials = partials;
+    a.g_dtype = g_dtype; a.partials = partials; a.loss = loss; a.stats = stats; a.ticket = ticket;
+    TRLX_REQUIRE(!ticket || (loss && stats), TRLX_ERR_ARG, "fused finalize needs loss and stats");
     hipLaunchKernelGGL(k_ppo_loss_elem, dim3(unsigned(trlx_ppo_loss_num_blocks(n))), dim3(kLossThreads), 0,
                        (hipStream_t)stream, a);
     return check_launch("k_ppo_loss_elem");

@@ -38,7 +38,7 @@ struct GaeArgs {
     const void* values;
     const void* rewards;
     int dtype;
-    int64_t B, T, Teff;
+    int B, T, Teff;
     float gamma, gl;  // gamma, gamma*lam (rounded to fp32 like the torch scalar)
     const float* lp;
     const float* ref_lp;
@@ -52,12 +52,27 @@ struct GaeArgs {
     void* rew_out;
     int rew_dtype;
     double* partials;
+    double* stats;       // optional: last block reduces the partials into stats[4]
+    unsigned* ticket;    // required with stats
     int rpb;     // rows per block
     int stride;  // LDS row stride (odd => conflict-free column walk)
 };
 
 constexpr int kGaeThreads = 256;
+constexpr int kGaeMaxRows = 16;      // rows per block: many small blocks, short staging loops
 constexpr int kGaeLdsFloats = 8192;  // per array (32 KB)
+
+// Fixed-order reduction of `n` partial records (TRLX_MOMENT_SLOTS doubles each) by one
+// block into out[TRLX_MOMENT_SLOTS].
+__device__ void reduce_moment_records(const double* partials, int n, double* out) {
+    __shared__ double red[TRLX_MOMENT_SLOTS][kMaxThreads / kWave];
+    double acc[TRLX_MOMENT_SLOTS] = {0, 0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) acc[k] += partials[i * TRLX_MOMENT_SLOTS + k];
+    for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) acc[k] = block_sum_d(acc[k], red[k]);
+    if (threadIdx.x == 0)
+        for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) out[k] = acc[k];
+}
 
 __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -65,18 +80,18 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
     float* sv = lds;                        // values, then returns
     float* sr = lds + a.rpb * a.stride;     // rewards, then advantages
     const int tid = threadIdx.x;
-    const int64_t row0 = int64_t(blockIdx.x) * a.rpb;
-    const int rows = int(min<int64_t>(a.rpb, a.B - row0));
-    const int64_t nel = int64_t(rows) * a.Teff;
+    const int row0 = blockIdx.x * a.rpb;
+    const int rows = min(a.rpb, a.B - row0);
+    const int nel = rows * a.Teff;
 
     // ---- stage values / rewards (coalesced: rows are contiguous with stride T)
     double msum = 0.0;
-    for (int64_t e = tid; e < nel; e += kGaeThreads) {
-        const int r = int(e / a.Teff);
-        const int64_t c = e - int64_t(r) * a.Teff;
-        const int64_t b = row0 + r;
-        const int64_t gi = b * a.T + c;
-        const int64_t len = a.lengths ? a.lengths[b] : a.T;
+    for (int e = tid; e < nel; e += kGaeThreads) {
+        const int r = e / a.Teff;
+        const int c = e - r * a.Teff;
+        const int b = row0 + r;
+        const int64_t gi = int64_t(b) * a.T + c;
+        const int len = a.lengths ? int(a.lengths[b]) : a.T;
         float v = 0.0f, rw = 0.0f;
         if (c < len) {
             v = ld_any(a.values, a.dtype, gi);
@@ -86,7 +101,7 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
         if (a.lp && a.rew_out) st_any(a.rew_out, a.rew_dtype, gi, rw);
         sv[r * a.stride + c] = v;
         sr[r * a.stride + c] = rw;
-        msum += a.mask ? double(a.mask[b * a.Teff + c]) : 1.0;
+        msum += a.mask ? double(a.mask[int64_t(b) * a.Teff + c]) : 1.0;
     }
     __syncthreads();
 
@@ -96,7 +111,7 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
         float* pv = sv + tid * a.stride;
         float* pr = sr + tid * a.stride;
         float A = 0.0f, vnext = 0.0f;
-        for (int64_t c = a.Teff - 1; c >= 0; --c) {
+        for (int c = a.Teff - 1; c >= 0; --c) {
             const float vcur = pv[c];
             const float nv = (c < a.Teff - 1) ? vnext : 0.0f;
             const float delta = add_rn(pr[c], mul_rn(a.gamma, nv)) - vcur;
@@ -113,10 +128,10 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
     msum = block_sum_d(msum, red[2]);  // (this barrier also orders the scan before the write-back)
 
     // ---- write back advantages (raw, fp32) and returns (coalesced)
-    for (int64_t e = tid; e < nel; e += kGaeThreads) {
-        const int r = int(e / a.Teff);
-        const int64_t c = e - int64_t(r) * a.Teff;
-        const int64_t oi = (row0 + r) * a.Teff + c;
+    for (int e = tid; e < nel; e += kGaeThreads) {
+        const int r = e / a.Teff;
+        const int c = e - r * a.Teff;
+        const int64_t oi = int64_t(row0 + r) * a.Teff + c;
         a.adv[oi] = sr[r * a.stride + c];
         st_any(a.ret, a.ret_dtype, oi, sv[r * a.stride + c]);
     }
@@ -127,12 +142,14 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
         p[2] = double(nel);
         p[3] = msum;
     }
+    if (a.stats && last_block_arrived(a.ticket, gridDim.x))
+        reduce_moment_records(a.partials, gridDim.x, a.stats);
 }
 
 static void gae_geometry(int64_t Teff, int& rpb, int& stride) {
     stride = int((Teff + 1) | 1);
     int64_t r = kGaeLdsFloats / stride;
-    if (r > 64) r = 64;
+    if (r > kGaeMaxRows) r = kGaeMaxRows;
     if (r < 1) r = 1;
     rpb = int(r);
 }
@@ -170,13 +187,7 @@ __global__ __launch_bounds__(kMomThreads) void k_moments_partial(const void* x, 
 
 __global__ __launch_bounds__(256) void k_moments_finalize(const double* partials, int64_t nblk,
                                                           double* stats) {
-    __shared__ double red[TRLX_MOMENT_SLOTS][256 / kWave];
-    double acc[TRLX_MOMENT_SLOTS] = {0, 0, 0, 0};
-    for (int64_t i = threadIdx.x; i < nblk; i += 256)
-        for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) acc[k] += partials[i * TRLX_MOMENT_SLOTS + k];
-    for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) acc[k] = block_sum_d(acc[k], red[k]);
-    if (threadIdx.x == 0)
-        for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) stats[k] = acc[k];
+    reduce_moment_records(partials, int(nblk), stats);
 }
 
 // ------------------------------------------------------------------ A4 whiten
@@ -233,19 +244,20 @@ extern "C" int trlx_gae_scan(const void* values, const void* rewards, int dtype,
                              const float* ref_lp, float neg_beta, const float* scores,
                              const int64_t* lengths, const int64_t* mask, float* adv_raw, void* ret,
                              int ret_dtype, void* rew_out, int rew_dtype, double* partials,
-                             void* stream) {
+                             double* stats, unsigned* ticket, void* stream) {
     TRLX_REQUIRE(values && adv_raw && ret && partials, TRLX_ERR_ARG, "NULL values/adv/ret/partials");
     TRLX_REQUIRE(rewards || (lp && ref_lp), TRLX_ERR_ARG, "need rewards or (lp, ref_lp)");
-    TRLX_REQUIRE(B > 0 && Teff > 0 && Teff <= T, TRLX_ERR_SHAPE, "bad shape B=%lld T=%lld Teff=%lld",
-                 (long long)B, (long long)T, (long long)Teff);
+    TRLX_REQUIRE(!stats || ticket, TRLX_ERR_ARG, "stats output needs a ticket word");
+    TRLX_REQUIRE(B > 0 && Teff > 0 && Teff <= T && B * T < (1LL << 31), TRLX_ERR_SHAPE,
+                 "bad shape B=%lld T=%lld Teff=%lld", (long long)B, (long long)T, (long long)Teff);
     TRLX_REQUIRE(!lp || Teff == T, TRLX_ERR_SHAPE, "fused KL reward needs response_length == T");
     GaeArgs a = {};
-    a.values = values; a.rewards = rewards; a.dtype = dtype; a.B = B; a.T = T; a.Teff = Teff;
+    a.values = values; a.rewards = rewards; a.dtype = dtype; a.B = int(B); a.T = int(T); a.Teff = int(Teff);
     a.gamma = gamma;
     a.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
     a.lp = lp; a.ref_lp = ref_lp; a.neg_beta = neg_beta; a.scores = scores; a.lengths = lengths;
     a.mask = mask; a.adv = adv_raw; a.ret = ret; a.ret_dtype = ret_dtype; a.rew_out = rew_out;
-    a.rew_dtype = rew_dtype; a.partials = partials;
+    a.rew_dtype = rew_dtype; a.partials = partials; a.stats = stats; a.ticket = ticket;
     gae_geometry(Teff, a.rpb, a.stride);
     const unsigned grid = unsigned((B + a.rpb - 1) / a.rpb);
     const size_t lds = size_t(2) * a.rpb * a.stride * sizeof(float);

@@ -8,6 +8,8 @@
 // token, never materialising the [B,T,V] log-softmax the reference builds
 // (trlx/utils/modeling.py:39).  No MFMA: there is no contraction on this path; the
 // roofline is HBM bandwidth.
+#include <string>
+
 #include "ppo_math.h"
 
 namespace trlx {
@@ -191,6 +193,166 @@ __global__ __launch_bounds__(kMaxThreads) void k_vocab_rows(RowArgs a) {
     if (jx >= 0) DT::store1(drow, jx, jx == y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
 }
 
+// ------------------------------------------------------------------ streaming variant
+// Same arithmetic, but the row is streamed through registers U vectors at a time with an
+// online (max, sum-exp) instead of being held whole: small register footprint => many
+// workgroups per CU keep loads continuously in flight.  Backward / fused modes make a
+// second pass over the row (served from L2 / the Infinity Cache when it was just read).
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+    const float nm = fmaxf(m, m2);
+    if (nm == -INFINITY) return;  // both empty
+    s = s * exp2_fast((m - nm) * kLog2e) + s2 * exp2_fast((m2 - nm) * kLog2e);
+    m = nm;
+}
+
+constexpr int kStreamMaxThreads = 256;  // launch bound of the streaming kernel (register budget)
+
+template <class DT, int U, int MODE>
+__global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs a) {
+    __shared__ float sh_m[kStreamMaxThreads / kWave];
+    __shared__ float sh_s[kStreamMaxThreads / kWave];
+    typedef typename DT::elem_t E;
+    constexpr int EPV = DT::kEPV;
+    const int64_t row = blockIdx.x;
+    const int64_t b = row / a.T, t = row - (row / a.T) * a.T;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const E* xrow = reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st;
+    const int64_t y = a.labels[b * a.lb + t * a.lt];
+    const bool y_ok = (y >= 0) && (y < a.V);
+    const RowSplit<DT> s(xrow, a.V);
+    const vec4u* vp = reinterpret_cast<const vec4u*>(xrow + s.head);
+    float ex = -INFINITY;
+    if (tid < s.head)
+        ex = DT::load1(xrow, tid);
+    else if (tid >= nthr - s.tail)
+        ex = DT::load1(xrow, s.tail0 + (tid - (nthr - s.tail)));
+    const float xy = y_ok ? DT::load1(xrow, y) : NAN;
+
+    float lse;
+    if (MODE == kBwd) {
+        lse = a.lse_in[row];
+    } else {
+        float m = ex, sum = (ex == -INFINITY) ? 0.0f : 1.0f;
+        for (int64_t base = tid; base < s.nvec; base += int64_t(nthr) * U) {
+            vec4u v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = base + int64_t(u) * nthr;
+                v[u] = (i < s.nvec) ? ld_stream(vp + i) : DT::neg_inf();
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float f[EPV];
+                DT::unpack(v[u], f);
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) mx = fmaxf(mx, f[e]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) launder(v[u]);
+            const float nm = fmaxf(m, mx);
+            if (nm == -INFINITY) continue;
+            sum *= exp2_fast((m - nm) * kLog2e);
+            const float nml2e = -nm * kLog2e;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float f[EPV];
+                DT::unpack(v[u], f);
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) sum += exp2_fast(fmaf(f[e], kLog2e, nml2e));
+            }
+            m = nm;
+        }
+        // wave combine, then fixed-order cross-wave combine
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float m2 = __shfl_xor(m, off, kWave), s2 = __shfl_xor(sum, off, kWave);
+            online_merge(m, sum, m2, s2);
+        }
+        if ((tid & (kWave - 1)) == 0) {
+            sh_m[tid / kWave] = m;
+            sh_s[tid / kWave] = sum;
+        }
+        __syncthreads();
+        m = sh_m[0];
+        sum = sh_s[0];
+        for (int w = 1; w < nthr / kWave; ++w) online_merge(m, sum, sh_m[w], sh_s[w]);
+        lse = m + logf(sum);
+    }
+    const float lp = xy - lse;
+    if (MODE == kFwd) {
+        if (tid == 0) {
+            void* out = blockIdx.y == 0 ? a.lp0 : a.lp1;
+            float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
+            st_any(out, a.out_dtype, row, lp);
+            if (lse_out) lse_out[row] = lse;
+        }
+        return;
+    }
+    float g;
+    if (MODE == kBwd) {
+        g = ld_any(a.grad, a.grad_dtype, row);
+    } else {
+        float A = a.adv[row];
+        if (a.stats) {
+            float mu, rstd;
+            whiten_coeffs(a.stats, a.unbiased, mu, rstd);
+            A = mul_rn(A - mu, rstd);
+        }
+        const float mval = a.mask ? float(a.mask[row]) : 1.0f;
+        const double msum = a.msum ? *a.msum : a.msum_host;
+        const float inv_msum = 1.0f / float(msum);
+        const float olp = ld_any(a.old_lp, a.old_dtype, row);
+        PolicyTerms pt;
+        g = ppo_policy_dlp(lp, olp, A, mval, inv_msum, a.cliprange, pt);
+        if (tid == 0) a.lp_out[row] = lp;
+    }
+    const float lse_l2e = -lse * kLog2e;
+    E* drow = reinterpret_cast<E*>(a.dx) + b * a.dsb + t * a.dst;
+    const float gy = g * (1.0f - exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
+    const bool same_phase = ((reinterpret_cast<uintptr_t>(drow) ^ reinterpret_cast<uintptr_t>(xrow)) & 15u) == 0;
+    const int64_t iy = y_ok && y >= s.head && y < s.tail0 ? (y - s.head) / EPV : -1;
+    vec4u* dvp = reinterpret_cast<vec4u*>(drow + s.head);
+    for (int64_t base = tid; base < s.nvec; base += int64_t(nthr) * U) {
+        vec4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + int64_t(u) * nthr;
+            if (i < s.nvec) v[u] = vp[i];  // second touch: cached read
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + int64_t(u) * nthr;
+            if (i >= s.nvec) continue;
+            float f[EPV];
+            DT::unpack(v[u], f);
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+            if (same_phase) {
+                if (i == iy) {
+                    const int ey = int(y - (s.head + i * EPV));
+#pragma unroll
+                    for (int e = 0; e < EPV; ++e)
+                        if (e == ey) f[e] = gy;
+                }
+                __builtin_nontemporal_store(DT::pack(f), dvp + i);
+            } else {
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) {
+                    const int64_t j = s.head + i * EPV + e;
+                    DT::store1(drow, j, j == y ? gy : f[e]);
+                }
+            }
+        }
+    }
+    int64_t jx = -1;
+    if (tid < s.head)
+        jx = tid;
+    else if (tid >= nthr - s.tail)
+        jx = s.tail0 + (tid - (nthr - s.tail));
+    if (jx >= 0) DT::store1(drow, jx, jx == y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+}
+
 // ------------------------------------------------------------------ launch geometry
 // Vectors per thread (NV) are compile-time so the row lives in registers; threads per
 // block = the smallest multiple of 64 that covers the row with NV vectors.
@@ -198,11 +360,19 @@ struct Geometry {
     int nv;
     int threads;
 };
+static int g_resident_threads = 0;  // preferred workgroup size for resident rows (0 = auto)
+
 static Geometry pick_geometry(int64_t V, int elem_bytes) {
     const int epv = 16 / elem_bytes;
     const int64_t nvec = V / epv + 1;
-    static const int kNV[] = {1, 2, 4, 8, 16};
+    static const int kNV[] = {1, 2, 4, 8, 13, 16};
+    if (g_resident_threads > 0) {  // fixed block size: smallest NV that covers the row
+        for (int nv : kNV)
+            if (nvec <= int64_t(nv) * g_resident_threads) return {nv, g_resident_threads};
+        return {0, 0};
+    }
     for (int nv : kNV) {
+        if (nv == 13) continue;
         if (nvec <= int64_t(nv) * kMaxThreads) {
             int64_t thr = (nvec + nv - 1) / nv;
             thr = ((thr + kWave - 1) / kWave) * kWave;
@@ -213,18 +383,34 @@ static Geometry pick_geometry(int64_t V, int elem_bytes) {
     return {0, 0};
 }
 
+// Tuning knobs (trlx_set_tuning): 0 = automatic.
+static int g_row_variant = 0;   // 1 = register-resident rows, 2 = streaming rows
+static int g_stream_threads = 0;
+static int g_stream_unroll = 0;
+
 template <int MODE, class DT>
 static int launch_rows_dt(const RowArgs& a, int nten, hipStream_t stream) {
-    const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t));
-    TRLX_REQUIRE(g.nv > 0, TRLX_ERR_SHAPE, "vocab size %lld too large for the register-resident row kernel",
-                 (long long)a.V);
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
+    const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t));
+    const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
+    if (variant == 2 || g.nv == 0) {
+        const int thr = g_stream_threads ? g_stream_threads : kStreamMaxThreads;
+        const int unroll = g_stream_unroll ? g_stream_unroll : 4;
+        if (unroll == 8)
+            hipLaunchKernelGGL((k_vocab_rows_stream<DT, 8, MODE>), grid, dim3(thr), 0, stream, a);
+        else if (unroll == 2)
+            hipLaunchKernelGGL((k_vocab_rows_stream<DT, 2, MODE>), grid, dim3(thr), 0, stream, a);
+        else
+            hipLaunchKernelGGL((k_vocab_rows_stream<DT, 4, MODE>), grid, dim3(thr), 0, stream, a);
+        return check_launch("k_vocab_rows_stream");
+    }
     const dim3 block(g.threads);
     switch (g.nv) {
         case 1: hipLaunchKernelGGL((k_vocab_rows<DT, 1, MODE>), grid, block, 0, stream, a); break;
         case 2: hipLaunchKernelGGL((k_vocab_rows<DT, 2, MODE>), grid, block, 0, stream, a); break;
         case 4: hipLaunchKernelGGL((k_vocab_rows<DT, 4, MODE>), grid, block, 0, stream, a); break;
         case 8: hipLaunchKernelGGL((k_vocab_rows<DT, 8, MODE>), grid, block, 0, stream, a); break;
+        case 13: hipLaunchKernelGGL((k_vocab_rows<DT, 13, MODE>), grid, block, 0, stream, a); break;
         default: hipLaunchKernelGGL((k_vocab_rows<DT, 16, MODE>), grid, block, 0, stream, a); break;
     }
     return check_launch("k_vocab_rows");
@@ -258,6 +444,7 @@ extern "C" int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype, in
     a.x0 = x0; a.x1 = x1; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
     a.labels = labels; a.lb = lb; a.lt = lt;
     a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype; a.lse0 = out_lse0; a.lse1 = out_lse1;
+    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;  // empty batch: nothing to launch
     int rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(out_lp0 && (!x1 || out_lp1), TRLX_ERR_ARG, "NULL logprob output");
@@ -272,6 +459,7 @@ extern "C" int trlx_lsm_gather_bwd(const void* x, int dtype, int64_t B, int64_t 
     RowArgs a = {};
     a.x0 = x; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
     a.lse_in = lse; a.grad = grad; a.grad_dtype = grad_dtype; a.dx = dx; a.dsb = dsb; a.dst = dst;
+    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;  // empty batch: nothing to launch
     int rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(lse && grad && dx, TRLX_ERR_ARG, "NULL lse/grad/dx");
@@ -289,9 +477,33 @@ extern "C" int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_
     a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv; a.stats = stats; a.unbiased = unbiased;
     a.mask = mask; a.msum = msum; a.msum_host = msum_host; a.cliprange = cliprange;
     a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
+    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;  // empty batch: nothing to launch
     int rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(old_lp && adv && lp_out && dx, TRLX_ERR_ARG, "NULL old_lp/adv/lp_out/dx");
     TRLX_REQUIRE(msum || msum_host > 0, TRLX_ERR_ARG, "mask sum must be positive");
     return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
+}
+
+extern "C" int trlx_set_tuning(const char* key, int64_t value) {
+    const std::string k = key ? key : "";
+    if (k == "row_variant") g_row_variant = int(value);
+    else if (k == "resident_threads") {
+        TRLX_REQUIRE(value == 0 || (value % kWave == 0 && value <= kMaxThreads), TRLX_ERR_ARG,
+                     "resident_threads must be a multiple of 64 <= %d", kMaxThreads);
+        g_resident_threads = int(value);
+    }
+    else if (k == "stream_threads") {
+        TRLX_REQUIRE(value == 0 || (value % kWave == 0 && value <= kStreamMaxThreads), TRLX_ERR_ARG,
+                     "stream_threads must be a multiple of 64 <= %d", kStreamMaxThreads);
+        g_stream_threads = int(value);
+    } else if (k == "stream_unroll") {
+        TRLX_REQUIRE(value == 0 || value == 2 || value == 4 || value == 8, TRLX_ERR_ARG, "stream_unroll: 2, 4 or 8");
+        g_stream_unroll = int(value);
+    }
+    else {
+        set_error("unknown tuning key '%s'", k.c_str());
+        return TRLX_ERR_ARG;
+    }
+    return TRLX_OK;
 }

@@ -135,13 +135,13 @@ class _PPOLoss(torch.autograd.Function):
         part = torch.empty(nblk * _lib.PPO_PARTIAL_SLOTS, dtype=torch.float64, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         stats = torch.empty(_lib.PPO_STATS, dtype=torch.float32, device=dev)
+        ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         _lib.call("trlx_ppo_loss_elem", n, _lib.ptr(lp), _lib.dtype_code(lp), _lib.ptr(v), _lib.dtype_code(v),
                   _lib.ptr(olp), _lib.dtype_code(olp), _lib.ptr(ov), _lib.dtype_code(ov),
                   _lib.ptr(adv), _lib.dtype_code(adv), None, 0, _lib.ptr(ret), _lib.dtype_code(ret),
                   _lib.ptr(m), _lib.ptr(msum_dev), float(n), float(c), float(cv), float(vf_coef),
-                  _lib.ptr(dlp), _lib.ptr(dv), _lib.F32, _lib.ptr(part), s)
-        _lib.call("trlx_ppo_loss_finalize", _lib.ptr(part), nblk, n, _lib.ptr(msum_dev), float(n),
-                  float(vf_coef), _lib.ptr(loss), _lib.ptr(stats), s)
+                  _lib.ptr(dlp), _lib.ptr(dv), _lib.F32, _lib.ptr(part), _lib.ptr(loss), _lib.ptr(stats),
+                  _lib.ptr(ticket), s)
         ctx.save_for_backward(dlp, dv)
         ctx.dtypes = (logprobs.dtype, values.dtype)
         ctx.shapes = (logprobs.shape, values.shape)
@@ -201,13 +201,13 @@ class _PPOLossFromLogits(torch.autograd.Function):
         part = torch.empty(nblk * _lib.PPO_PARTIAL_SLOTS, dtype=torch.float64, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         stats = torch.empty(_lib.PPO_STATS, dtype=torch.float32, device=dev)
+        ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         _lib.call("trlx_ppo_loss_elem", n, _lib.ptr(lp_new), _lib.F32, _lib.ptr(v), _lib.dtype_code(v),
                   _lib.ptr(olp), _lib.dtype_code(olp), _lib.ptr(ov), _lib.dtype_code(ov),
                   _lib.ptr(adv), _lib.F32, _lib.ptr(adv_stats), int(unbiased), _lib.ptr(ret),
                   _lib.dtype_code(ret), _lib.ptr(m), _lib.ptr(msum_dev), float(n), float(c), float(cv),
-                  float(vf_coef), None, _lib.ptr(dv), _lib.F32, _lib.ptr(part), s)
-        _lib.call("trlx_ppo_loss_finalize", _lib.ptr(part), nblk, n, _lib.ptr(msum_dev), float(n),
-                  float(vf_coef), _lib.ptr(loss), _lib.ptr(stats), s)
+                  float(vf_coef), None, _lib.ptr(dv), _lib.F32, _lib.ptr(part), _lib.ptr(loss),
+                  _lib.ptr(stats), _lib.ptr(ticket), s)
         ctx.save_for_backward(dv)
         ctx.dx = dx
         ctx.shapes = (logits.shape, lg is logits, values.shape, values.dtype)
@@ -284,10 +284,11 @@ class PPOConfig:
         st = torch.empty(_lib.MOMENT_SLOTS, dtype=torch.float64, device=dev)
         ln = None if lengths is None else lengths.to(device=dev, dtype=torch.int64).contiguous()
         mk = None if mask is None else mask.to(device=dev, dtype=torch.int64).contiguous()
+        ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         _lib.call("trlx_gae_scan", _lib.ptr(v), _lib.ptr(r), _lib.dtype_code(v), B, T, L, float(self.gamma),
                   float(self.lam), None, None, 0.0, None, _lib.ptr(ln), _lib.ptr(mk), _lib.ptr(adv),
-                  _lib.ptr(ret), _lib.dtype_code(ret), None, _lib.F32, _lib.ptr(part), s)
-        _lib.call("trlx_moments_finalize", _lib.ptr(part), nblk, _lib.ptr(st), s)
+                  _lib.ptr(ret), _lib.dtype_code(ret), None, _lib.F32, _lib.ptr(part), _lib.ptr(st),
+                  _lib.ptr(ticket), s)
         return adv, ret, st
 
     def get_advantages_and_returns(self, values: torch.Tensor, rewards: torch.Tensor, response_length: int,

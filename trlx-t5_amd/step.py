@@ -5,16 +5,15 @@ One `PPOHotPath.step` is, per response token of the shard:
   experience (ppo_orchestrator.py:154-167)
     K1  trlx_lsm_gather_fwd    policy + reference logits rows -> lp, ref_lp      (2 x V*s read)
   loss side (accelerate_ppo_model.py:88-126 -> ppo_models.py:121-199)
-    K2  trlx_gae_scan          KL reward (fused) + GAE reverse scan + whitening moments
-    K3  trlx_moments_finalize  fixed-order reduction of the moments
+    K2  trlx_gae_scan          KL reward (fused) + GAE reverse scan + whitening moments,
+                               last block reduces the moments (fixed order)
         [RCCL all-reduce of {sum A, sum A^2, n} when world > 1 — the only exchange]
-    K4  trlx_ppo_policy_fused  new-policy logits rows -> lp_new, PPO policy grad, dlogits
+    K3  trlx_ppo_policy_fused  new-policy logits rows -> lp_new, PPO policy grad, dlogits
                                (1 x V*s read + 1 x V*s write)
-    K5  trlx_ppo_loss_elem     value loss + grads, stats partials
-    K6  trlx_ppo_loss_finalize loss + 13 stats
+    K4  trlx_ppo_loss_elem     value loss + grads + stats partials; last block -> loss, 13 stats
         [RCCL all-reduce of the stats vector for logging when world > 1]
 
-Buffers are allocated once per shape; the step launches six kernels and allocates
+Buffers are allocated once per shape; the step launches four kernels and allocates
 nothing.  Rows (rollouts) are sharded contiguously across ranks by the caller
 (accelerate_ppo_model.py:146-148 semantics); reference-exact normalisers stay rank-local.
 """
@@ -52,6 +51,7 @@ class PPOHotPath:
         self.n_loss = _lib.query("trlx_ppo_loss_num_blocks", B * T)
         self.loss_part = torch.empty(self.n_loss * _lib.PPO_PARTIAL_SLOTS, dtype=torch.float64, device=self.device)
         self.loss = torch.empty(1, **f32)
+        self.tickets = torch.zeros(2, dtype=torch.int32, device=self.device)  # re-armed by the kernels
         self.stats = torch.empty(_lib.PPO_STATS, **f32)
         self.dlogits = None
         self.timers = None  # optional {name: [(start_event, end_event), ...]}
@@ -104,9 +104,7 @@ class PPOHotPath:
                   float(self.cfg.gamma), float(self.cfg.lam), self.lp_old.data_ptr(), self.ref_lp.data_ptr(),
                   -self.kl_coef, _lib.ptr(scores), _lib.ptr(lengths), _lib.ptr(mask), self.adv_raw.data_ptr(),
                   self.returns.data_ptr(), _lib.dtype_code(self.returns), self.rewards.data_ptr(), _lib.F32,
-                  self.gae_part.data_ptr(), s.cuda_stream)
-        _lib.call("trlx_moments_finalize", self.gae_part.data_ptr(), self.n_gae, self.adv_stats.data_ptr(),
-                  s.cuda_stream)
+                  self.gae_part.data_ptr(), self.adv_stats.data_ptr(), self.tickets[0:1].data_ptr(), s.cuda_stream)
         self._ev_end("gae", s)
         self.distributed = dist.is_available() and dist.is_initialized()
         if self.distributed:
@@ -139,9 +137,7 @@ class PPOHotPath:
                   unbiased, self.returns.data_ptr(), _lib.dtype_code(self.returns), _lib.ptr(mask),
                   msum.data_ptr(), float(n), float(self.cfg.cliprange), float(self.cfg.cliprange_value),
                   float(self.cfg.vf_coef), None, self.dvalues.data_ptr(), _lib.F32, self.loss_part.data_ptr(),
-                  s.cuda_stream)
-        _lib.call("trlx_ppo_loss_finalize", self.loss_part.data_ptr(), self.n_loss, n, msum.data_ptr(), float(n),
-                  float(self.cfg.vf_coef), self.loss.data_ptr(), self.stats.data_ptr(), s.cuda_stream)
+                  self.loss.data_ptr(), self.stats.data_ptr(), self.tickets[1:2].data_ptr(), s.cuda_stream)
         self._ev_end("loss_stats", s)
         return self.loss, self.stats, self.dlogits, self.dvalues
 
