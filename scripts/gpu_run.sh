@@ -24,6 +24,7 @@ for step in "$@"; do
         testsall) run gpu_tests 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
         sweep) run sweep 300 python tools/row_sweep.py ;;
         sweep_c4) B=128 T=128 V=32128 run sweep_c4 300 python tools/row_sweep.py ;;
+        sweep_f32) DT=f32 run sweep_f32 300 python tools/row_sweep.py ;;
         bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;
         bench_c3) run bench_c3 300 python bench.py --steps 20 --warmup 5 --config c3 --cpu-seconds 0 ;;
         bench_c4) run bench_c4 300 python bench.py --steps 20 --warmup 5 --config c4 --cpu-seconds 0 ;;

@@ -38,17 +38,11 @@ def main():
                   y.data_ptr(), y.stride(0), y.stride(1), lp1.data_ptr(), _lib.F32, adv.data_ptr(), None, 1, None,
                   None, float(B * T), 0.2, lp0.data_ptr(), dx.data_ptr(), dx.stride(0), dx.stride(1), s)
 
-    variants = [
-        ("resident auto", dict(row_variant=1, resident_threads=0)),
-        ("resident 512", dict(row_variant=1, resident_threads=512)),
-        ("resident 1024", dict(row_variant=1, resident_threads=1024)),
-        ("resident 256", dict(row_variant=1, resident_threads=256)),
-        ("stream 256 u2", dict(row_variant=2, stream_threads=256, stream_unroll=2)),
-        ("stream 256 u4", dict(row_variant=2, stream_threads=256, stream_unroll=4)),
-        ("stream 256 u8", dict(row_variant=2, stream_threads=256, stream_unroll=8)),
-        ("stream 128 u4", dict(row_variant=2, stream_threads=128, stream_unroll=4)),
-        ("stream 64 u8", dict(row_variant=2, stream_threads=64, stream_unroll=8)),
-    ]
+    variants = [("resident auto", dict(row_variant=1))]
+    for thr in (384, 448, 512, 576, 640, 768, 1024):
+        variants.append((f"resident {thr}", dict(row_variant=1, resident_threads=thr)))
+    for thr, u in ((256, 2), (256, 4), (256, 8), (128, 8)):
+        variants.append((f"stream {thr} u{u}", dict(row_variant=2, stream_threads=thr, stream_unroll=u)))
 
     def setv(cfg):
         for k in ("row_variant", "resident_threads", "stream_threads", "stream_unroll"):

@@ -107,30 +107,72 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
     return r;
 }
 
-// ------------------------------------------------------------------ last-block hand-off
-// Returns true (in every thread) in the one block of the grid that arrives last; all other
-// blocks' prior global stores are then visible to that block.  Protocol of
-// MI355X_MICROARCH.md "Valid forms" (producer: plain stores -> every wave vmcnt(0) ->
-// barrier -> lane-0 agent release fence -> asm vmcnt(0) -> agent atomic; consumer:
-// agent acquire fence -> vmcnt(0) -> barrier -> plain loads).  `ticket` must be 0 at
-// launch; the last block re-arms it to 0 for the next (stream-ordered) launch.
-__device__ __forceinline__ bool last_block_arrived(unsigned* ticket, unsigned nblocks) {
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// K independent fp64 sums over the block with ONE barrier: shuffle-reduce inside each
+// wave (the K chains interleave), lane 0 of each wave parks its K sums in LDS, then
+// thread k < K adds the waves' sums in fixed order.  Result valid in threads k < K only
+// (out_k).  `sh` holds (blockDim.x/64) * K doubles.  Deterministic.
+template <int K>
+__device__ __forceinline__ double block_sum_multi(const double (&v)[K], double* sh) {
+    double w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = v[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < K; ++k) w[k] += __shfl_xor(w[k], off, kWave);
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wv * K + k] = w[k];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    double r = 0.0;
+    if (threadIdx.x < K) {
+        const int nw = blockDim.x / kWave;
+        r = sh[threadIdx.x];
+        for (int i = 1; i < nw; ++i) r += sh[i * K + threadIdx.x];
+    }
+    return r;
+}
+
+// ------------------------------------------------------------------ last-block hand-off
+// Block-level partial record -> the block that arrives last reduces all records.
+// Fence-free form of MI355X_MICROARCH.md "Valid forms", table row 1: every payload byte
+// is stored write-through (`sc1`: relaxed agent-scope atomic stores) by the storing wave,
+// which drains them (`s_waitcnt vmcnt(0)`) before ONE lane adds to the unsharded ticket;
+// the block whose add returns nblocks-1 is last and reads every record with `sc1` loads
+// (relaxed agent-scope atomic loads), so no release/acquire fence (~1.7 us each) is paid.
+// The record's K values live in threads k < K of wave 0 (block_sum_multi's layout).
+// `ticket` must be 0 at launch; the last block re-arms it to 0.
+template <int K>
+__device__ __forceinline__ bool publish_record_last(double* rec, double val, unsigned* ticket,
+                                                    unsigned nblocks) {
+    static_assert(K <= kWave, "record must be stored by wave 0");
+    __shared__ int s_last;
+    if (threadIdx.x < kWave) {  // wave 0 stores and signals
+        if (threadIdx.x < K) __hip_atomic_store(rec + threadIdx.x, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (t == nblocks - 1);
-        if (s_last) {
-            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) {
+            const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = (t == nblocks - 1);
+            if (s_last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
     return s_last != 0;
+}
+
+// Fixed-order sum of `n` records of K doubles read with sc1 loads (see above); the sums
+// end up in threads k < K (block_sum_multi layout).  `sh`: (blockDim.x/64) * K doubles.
+template <int K>
+__device__ __forceinline__ double reduce_records(const double* recs, int n, double* sh) {
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            acc[k] += __hip_atomic_load(recs + int64_t(i) * K + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return block_sum_multi<K>(acc, sh);
 }
 
 // ------------------------------------------------------------------ 16-byte row vectors

@@ -27,23 +27,23 @@ constexpr int kLossThreads = 256;
 constexpr int kLossPerBlock = kLossThreads * 2;  // many short blocks: latency, not bandwidth, bound
 constexpr int kSlots = TRLX_PPO_PARTIAL_SLOTS;
 
-// One block: fixed-order sum of the partial records, then the loss and the 13 stats
-// (ppo_models.py:162-198; the divisions by N are torch.mean, var is unbiased).
-__device__ void ppo_loss_reduce(const double* partials, int nblk, int64_t n, double msum, float vf_coef,
-                                float* loss, float* stats) {
-    __shared__ double red[kSlots][kMaxThreads / kWave];
-    double acc[kSlots];
-    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
-    for (int i = threadIdx.x; i < nblk; i += blockDim.x)
-        for (int k = 0; k < kSlots; ++k) acc[k] += partials[int64_t(i) * kSlots + k];
-    for (int k = 0; k < kSlots; ++k) acc[k] = block_sum_d(acc[k], red[k]);
+// Loss and the 13 stats from the fixed-order totals of the records (ppo_models.py:162-198;
+// the divisions by N are torch.mean, var is unbiased).  `tot` lives in threads k < kSlots
+// (block_sum_multi layout); thread 0 gathers them through `sh`.
+__device__ void ppo_loss_emit(double tot, int64_t n, double msum, float vf_coef, float* loss, float* stats,
+                              double* sh) {
+    __syncthreads();
+    if (threadIdx.x < kSlots) sh[threadIdx.x] = tot;
+    __syncthreads();
     if (threadIdx.x != 0) return;
+    double acc[kSlots];
+    for (int k = 0; k < kSlots; ++k) acc[k] = sh[k];
     const double N = double(n);
     const double vf = 0.5 * acc[0] / msum;
     const double pg = acc[3] / msum;
-    const double tot = pg + double(vf_coef) * vf;
-    loss[0] = float(tot);
-    stats[0] = float(tot);                                  // losses/total_loss
+    const double total = pg + double(vf_coef) * vf;
+    loss[0] = float(total);
+    stats[0] = float(total);                                // losses/total_loss
     stats[1] = float(pg);                                   // losses/policy_loss
     stats[2] = float(vf);                                   // losses/value_loss
     stats[3] = float(acc[5] / N);                           // values/mean_old_values
@@ -59,7 +59,7 @@ __device__ void ppo_loss_reduce(const double* partials, int nblk, int64_t n, dou
 }
 
 __global__ __launch_bounds__(kLossThreads) void k_ppo_loss_elem(LossArgs a) {
-    __shared__ double red[kSlots][kLossThreads / kWave];
+    __shared__ double red[(kLossThreads / kWave) * kSlots];
     const int64_t beg = int64_t(blockIdx.x) * kLossPerBlock;
     const int64_t end = min<int64_t>(a.n, beg + kLossPerBlock);
     float mu = 0.f, rstd = 1.f;
@@ -120,21 +120,25 @@ __global__ __launch_bounds__(kLossThreads) void k_ppo_loss_elem(LossArgs a) {
         acc[11] += double(mul_rn(pt.ratio, m));
         acc[12] += double(m);
     }
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k) acc[k] = block_sum_d(acc[k], red[k]);
-    if (threadIdx.x == 0) {
-        double* p = a.partials + blockIdx.x * kSlots;
-#pragma unroll
-        for (int k = 0; k < kSlots; ++k) p[k] = acc[k];
+    const double rec = block_sum_multi<kSlots>(acc, red);
+    double* my = a.partials + blockIdx.x * kSlots;
+    if (!a.ticket) {
+        if (threadIdx.x < kSlots) my[threadIdx.x] = rec;
+        return;
     }
-    if (a.ticket && last_block_arrived(a.ticket, gridDim.x))
-        ppo_loss_reduce(a.partials, gridDim.x, a.n, msum, a.vf_coef, a.loss, a.stats);
+    if (publish_record_last<kSlots>(my, rec, a.ticket, gridDim.x)) {
+        __syncthreads();  // red[] reuse
+        const double tot = reduce_records<kSlots>(a.partials, gridDim.x, red);
+        ppo_loss_emit(tot, a.n, msum, a.vf_coef, a.loss, a.stats, red);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_ppo_loss_finalize(const double* partials, int64_t nblk, int64_t n,
                                                            const double* msum_p, double msum_host,
                                                            float vf_coef, float* loss, float* stats) {
-    ppo_loss_reduce(partials, int(nblk), n, msum_p ? *msum_p : msum_host, vf_coef, loss, stats);
+    __shared__ double red[(256 / kWave) * kSlots];
+    const double tot = reduce_records<kSlots>(partials, int(nblk), red);
+    ppo_loss_emit(tot, n, msum_p ? *msum_p : msum_host, vf_coef, loss, stats, red);
 }
 
 // ------------------------------------------------------------------ autograd scaling

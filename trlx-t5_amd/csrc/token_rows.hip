@@ -62,21 +62,9 @@ constexpr int kGaeThreads = 256;
 constexpr int kGaeMaxRows = 16;      // rows per block: many small blocks, short staging loops
 constexpr int kGaeLdsFloats = 8192;  // per array (32 KB)
 
-// Fixed-order reduction of `n` partial records (TRLX_MOMENT_SLOTS doubles each) by one
-// block into out[TRLX_MOMENT_SLOTS].
-__device__ void reduce_moment_records(const double* partials, int n, double* out) {
-    __shared__ double red[TRLX_MOMENT_SLOTS][kMaxThreads / kWave];
-    double acc[TRLX_MOMENT_SLOTS] = {0, 0, 0, 0};
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
-        for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) acc[k] += partials[i * TRLX_MOMENT_SLOTS + k];
-    for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) acc[k] = block_sum_d(acc[k], red[k]);
-    if (threadIdx.x == 0)
-        for (int k = 0; k < TRLX_MOMENT_SLOTS; ++k) out[k] = acc[k];
-}
-
 __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ double red[3][kGaeThreads / kWave];
+    __shared__ double red[(kGaeThreads / kWave) * TRLX_MOMENT_SLOTS];
     float* sv = lds;                        // values, then returns
     float* sr = lds + a.rpb * a.stride;     // rewards, then advantages
     const int tid = threadIdx.x;
@@ -123,9 +111,9 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
             s2 += double(A) * double(A);
         }
     }
-    s1 = block_sum_d(s1, red[0]);
-    s2 = block_sum_d(s2, red[1]);
-    msum = block_sum_d(msum, red[2]);  // (this barrier also orders the scan before the write-back)
+    const double mine[TRLX_MOMENT_SLOTS] = {s1, s2, double(tid == 0 ? nel : 0), msum};
+    const double rec = block_sum_multi<TRLX_MOMENT_SLOTS>(mine, red);  // (its barrier also orders
+                                                                      //  the scan before write-back)
 
     // ---- write back advantages (raw, fp32) and returns (coalesced)
     for (int e = tid; e < nel; e += kGaeThreads) {
@@ -135,15 +123,16 @@ __global__ __launch_bounds__(kGaeThreads) void k_gae(GaeArgs a) {
         a.adv[oi] = sr[r * a.stride + c];
         st_any(a.ret, a.ret_dtype, oi, sv[r * a.stride + c]);
     }
-    if (tid == 0) {
-        double* p = a.partials + blockIdx.x * TRLX_MOMENT_SLOTS;
-        p[0] = s1;
-        p[1] = s2;
-        p[2] = double(nel);
-        p[3] = msum;
+    double* my = a.partials + blockIdx.x * TRLX_MOMENT_SLOTS;
+    if (!a.stats) {
+        if (tid < TRLX_MOMENT_SLOTS) my[tid] = rec;
+        return;
     }
-    if (a.stats && last_block_arrived(a.ticket, gridDim.x))
-        reduce_moment_records(a.partials, gridDim.x, a.stats);
+    if (publish_record_last<TRLX_MOMENT_SLOTS>(my, rec, a.ticket, gridDim.x)) {
+        __syncthreads();  // red[] reuse
+        const double tot = reduce_records<TRLX_MOMENT_SLOTS>(a.partials, gridDim.x, red);
+        if (tid < TRLX_MOMENT_SLOTS) a.stats[tid] = tot;
+    }
 }
 
 static void gae_geometry(int64_t Teff, int& rpb, int& stride) {
@@ -165,7 +154,7 @@ __device__ __forceinline__ double ld_moment(const void* p, int dtype, int64_t i)
 
 __global__ __launch_bounds__(kMomThreads) void k_moments_partial(const void* x, int dtype, int64_t n,
                                                                  double* partials) {
-    __shared__ double red[2][kMomThreads / kWave];
+    __shared__ double red[(kMomThreads / kWave) * TRLX_MOMENT_SLOTS];
     const int64_t beg = int64_t(blockIdx.x) * kMomPerBlock;
     const int64_t end = min<int64_t>(n, beg + kMomPerBlock);
     double s1 = 0.0, s2 = 0.0;
@@ -174,20 +163,16 @@ __global__ __launch_bounds__(kMomThreads) void k_moments_partial(const void* x, 
         s1 += v;
         s2 += v * v;
     }
-    s1 = block_sum_d(s1, red[0]);
-    s2 = block_sum_d(s2, red[1]);
-    if (threadIdx.x == 0) {
-        double* p = partials + blockIdx.x * TRLX_MOMENT_SLOTS;
-        p[0] = s1;
-        p[1] = s2;
-        p[2] = double(end - beg);
-        p[3] = 0.0;
-    }
+    const double mine[TRLX_MOMENT_SLOTS] = {s1, s2, threadIdx.x == 0 ? double(end - beg) : 0.0, 0.0};
+    const double rec = block_sum_multi<TRLX_MOMENT_SLOTS>(mine, red);
+    if (threadIdx.x < TRLX_MOMENT_SLOTS) partials[blockIdx.x * TRLX_MOMENT_SLOTS + threadIdx.x] = rec;
 }
 
 __global__ __launch_bounds__(256) void k_moments_finalize(const double* partials, int64_t nblk,
                                                           double* stats) {
-    reduce_moment_records(partials, int(nblk), stats);
+    __shared__ double red[(256 / kWave) * TRLX_MOMENT_SLOTS];
+    const double tot = reduce_records<TRLX_MOMENT_SLOTS>(partials, int(nblk), red);
+    if (threadIdx.x < TRLX_MOMENT_SLOTS) stats[threadIdx.x] = tot;
 }
 
 // ------------------------------------------------------------------ A4 whiten

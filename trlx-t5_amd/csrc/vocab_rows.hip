@@ -362,23 +362,26 @@ struct Geometry {
 };
 static int g_resident_threads = 0;  // preferred workgroup size for resident rows (0 = auto)
 
-static Geometry pick_geometry(int64_t V, int elem_bytes) {
+// Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
+// workgroup size.  Default: 512-thread workgroups (8 waves) -- measured on MI355X (C2,
+// bf16 V=50257) to keep 3 rows in flight per CU at ~71 VGPRs, 6.7 TB/s for the forward;
+// rows too long for 16 vectors x 512 threads use 1024 threads, then the streaming kernel.
+static const int kNVs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 16};
+
+static Geometry pick_geometry(int64_t V, int elem_bytes, bool allow_1024) {
     const int epv = 16 / elem_bytes;
-    const int64_t nvec = V / epv + 1;
-    static const int kNV[] = {1, 2, 4, 8, 13, 16};
-    if (g_resident_threads > 0) {  // fixed block size: smallest NV that covers the row
-        for (int nv : kNV)
-            if (nvec <= int64_t(nv) * g_resident_threads) return {nv, g_resident_threads};
-        return {0, 0};
-    }
-    for (int nv : kNV) {
-        if (nv == 13) continue;
-        if (nvec <= int64_t(nv) * kMaxThreads) {
+    const int64_t nvec = V / epv + 1;  // upper bound incl. head/tail peeling
+    const int prefs[2] = {g_resident_threads > 0 ? g_resident_threads : 512, kMaxThreads};
+    for (int pi = 0; pi < (allow_1024 ? 2 : 1); ++pi) {
+        const int pref = prefs[pi];
+        const int64_t need = (nvec + pref - 1) / pref;
+        for (int nv : kNVs) {
+            if (nv < need) continue;
             int64_t thr = (nvec + nv - 1) / nv;
             thr = ((thr + kWave - 1) / kWave) * kWave;
-            if (thr < 256 && nv > 1) continue;  // prefer >= 4 waves per row before deepening
             return {nv, int(thr < kWave ? kWave : thr)};
         }
+        if (g_resident_threads > 0) break;  // a fixed size that does not fit -> streaming
     }
     return {0, 0};
 }
@@ -391,7 +394,10 @@ static int g_stream_unroll = 0;
 template <int MODE, class DT>
 static int launch_rows_dt(const RowArgs& a, int nten, hipStream_t stream) {
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
-    const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t));
+    // Forward (read-only): resident rows while a 512-thread workgroup holds the row, else
+    // streaming (measured: 1024-thread resident rows lose ~20% to streaming on fp32 V=50257).
+    // Backward / fused (read + write): resident up to 1024 threads (one read instead of two).
+    const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
     if (variant == 2 || g.nv == 0) {
         const int thr = g_stream_threads ? g_stream_threads : kStreamMaxThreads;
@@ -405,14 +411,15 @@ static int launch_rows_dt(const RowArgs& a, int nten, hipStream_t stream) {
         return check_launch("k_vocab_rows_stream");
     }
     const dim3 block(g.threads);
+#define TRLX_RESIDENT_CASE(N) \
+    case N: hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE>), grid, block, 0, stream, a); break;
     switch (g.nv) {
-        case 1: hipLaunchKernelGGL((k_vocab_rows<DT, 1, MODE>), grid, block, 0, stream, a); break;
-        case 2: hipLaunchKernelGGL((k_vocab_rows<DT, 2, MODE>), grid, block, 0, stream, a); break;
-        case 4: hipLaunchKernelGGL((k_vocab_rows<DT, 4, MODE>), grid, block, 0, stream, a); break;
-        case 8: hipLaunchKernelGGL((k_vocab_rows<DT, 8, MODE>), grid, block, 0, stream, a); break;
-        case 13: hipLaunchKernelGGL((k_vocab_rows<DT, 13, MODE>), grid, block, 0, stream, a); break;
-        default: hipLaunchKernelGGL((k_vocab_rows<DT, 16, MODE>), grid, block, 0, stream, a); break;
+        TRLX_RESIDENT_CASE(1) TRLX_RESIDENT_CASE(2) TRLX_RESIDENT_CASE(3) TRLX_RESIDENT_CASE(4)
+        TRLX_RESIDENT_CASE(5) TRLX_RESIDENT_CASE(6) TRLX_RESIDENT_CASE(7) TRLX_RESIDENT_CASE(8)
+        TRLX_RESIDENT_CASE(10) TRLX_RESIDENT_CASE(12) TRLX_RESIDENT_CASE(13) TRLX_RESIDENT_CASE(16)
+        default: TRLX_REQUIRE(false, TRLX_ERR_SHAPE, "no resident geometry for NV=%d", g.nv);
     }
+#undef TRLX_RESIDENT_CASE
     return check_launch("k_vocab_rows");
 }
 
