@@ -46,12 +46,14 @@ def parse():
 
 
 def algorithmic_bytes(V, s, masked):
-    """Minimum HBM bytes per response token, per kernel."""
-    exp = 2 * V * s + 8 + 2 * 4                  # policy+ref rows, label, lp + ref_lp out
-    loss = 2 * V * s + 8 + 4 + 4 + 4 + (8 if masked else 0)  # row read + dlogits write, label, old_lp, adv, lp out
-    small = 4 * 4 + 4 * 2 + 4 + 4 * 2 + 4        # gae: values, lp, ref_lp, rewards/adv/ret out ...
-    stats = 4 * 6 + 4                            # loss elem: lp_new, v, old_lp, ov, adv, ret -> dv
-    return {"experience_lsm": exp, "loss_fused": loss, "step": exp + loss + small + stats}
+    """Minimum HBM bytes per response token, per launch.  Each [B,T] fp32
+    vector read or written once counts 4 B; int64 labels / mask 8 B."""
+    mask_b = 8 if masked else 0
+    # K1: policy + ref rows, label; out lp, ref_lp; tail: values in, rewards/adv/returns out
+    exp = 2 * V * s + 8 + 2 * 4 + 4 + 3 * 4 + mask_b
+    # K2: row read + dlogits write, label, old_lp, adv, values, old_values, returns in; lp, dv out
+    loss = 2 * V * s + 8 + 4 * 6 + 2 * 4 + mask_b
+    return {"experience": exp, "loss": loss, "step": exp + loss}
 
 
 def make_inputs(torch, B, T, V, dev, seed, masked):
@@ -162,7 +164,7 @@ def main():
     ab = algorithmic_bytes(V, 2, masked)
     roof = None
     if kern_ms:
-        dom = max(("experience_lsm", "loss_fused"), key=lambda k: kern_ms.get(k, 0.0))
+        dom = max(("experience", "loss"), key=lambda k: kern_ms.get(k, 0.0))
         ach = ab[dom] * tokens / (kern_ms[dom] * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")

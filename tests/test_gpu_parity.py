@@ -363,14 +363,41 @@ def test_hot_path_step_vs_oracle(B, Tn, V, lengths):
     assert row_sum.abs().max().item() < 1e-3
 
 
-def test_hot_path_step_is_deterministic():
+def test_hot_path_step_is_deterministic_and_rearms():
+    """Same inputs -> bitwise-identical outputs, across fresh instances and across repeated
+    steps of one instance (the in-kernel arrival tickets re-arm themselves)."""
     args = _step_inputs(32, 48, 50257, 11)
     logits, ref_logits, new_logits, labels, old_values, values, scores, _, _ = args
     d = [cuda(t) for t in (logits, ref_logits, new_logits, labels, old_values, values, scores)]
     outs = []
-    for _ in range(2):
-        hp = P.PPOHotPath(P.PPOConfig(), 32, 48, 50257, torch.bfloat16, DEV, kl_coef=0.05)
+    hp = P.PPOHotPath(P.PPOConfig(), 32, 48, 50257, torch.bfloat16, DEV, kl_coef=0.05)
+    for i in range(4):
+        if i == 3:
+            hp = P.PPOHotPath(P.PPOConfig(), 32, 48, 50257, torch.bfloat16, DEV, kl_coef=0.05)
         loss, stats, dl, dv = hp.step(*d)
-        outs.append((loss.clone(), stats.clone(), dl.clone(), dv.clone()))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+        outs.append((loss.clone(), stats.clone(), dl.clone(), dv.clone(), hp.adv_stats.clone(), hp.returns.clone()))
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
+    assert int(hp.workspace.view(torch.int32)[:2 * (32 + 1) + 2].abs().sum()) == 0  # tickets re-armed
+
+
+@pytest.mark.parametrize("T", [1, 63, 64, 65, 130])
+def test_fused_experience_tail_chunking(T):
+    """The lane-parallel GAE scan in the experience tail across 64-token chunk boundaries."""
+    B, V = 6, 257
+    logits, ref_logits, new_logits, labels, old_values, values, scores, L, mask = _step_inputs(B, T, V, 77 + T,
+                                                                                               lengths=T > 1)
+    hp = P.PPOHotPath(P.PPOConfig(gamma=0.99), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    hp.step(cuda(logits), cuda(ref_logits), cuda(new_logits), cuda(labels), cuda(old_values), cuda(values),
+            cuda(scores), lengths=None if L is None else cuda(L), mask=None if mask is None else cuda(mask))
+    torch.cuda.synchronize()
+    ref = orc.ppo_step_reference(logits.float(), ref_logits.float(), new_logits.float(), labels, old_values,
+                                 values, scores, cfg_kwargs=dict(gamma=0.99), kl_coef=0.05, lengths=L, mask=mask)
+    torch.testing.assert_close(hp.rewards.cpu(), ref["rewards"], **RT32)
+    torch.testing.assert_close(hp.returns.cpu(), ref["returns"], rtol=1e-5, atol=2e-5)
+    if B * T > 1:
+        mu = hp.adv_stats[0].item() / hp.adv_stats[2].item()
+        torch.testing.assert_close(torch.tensor(mu), (ref["returns"] - (old_values if L is None else
+                                   old_values.masked_fill(mask == 0, 0))).mean().double().float(),
+                                   rtol=1e-4, atol=1e-5)

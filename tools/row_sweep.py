@@ -38,8 +38,8 @@ def main():
                   y.data_ptr(), y.stride(0), y.stride(1), lp1.data_ptr(), _lib.F32, adv.data_ptr(), None, 1, None,
                   None, float(B * T), 0.2, lp0.data_ptr(), dx.data_ptr(), dx.stride(0), dx.stride(1), s)
 
-    variants = [("resident auto", dict(row_variant=1))]
-    for thr in (384, 448, 512, 576, 640, 768, 1024):
+    variants = [("resident auto", dict(row_variant=1)), ("resident 512 nolb", dict(row_variant=1, resident_lb512=0))]
+    for thr in (448, 512, 640, 1024):
         variants.append((f"resident {thr}", dict(row_variant=1, resident_threads=thr)))
     for thr, u in ((256, 2), (256, 4), (256, 8), (128, 8)):
         variants.append((f"stream {thr} u{u}", dict(row_variant=2, stream_threads=thr, stream_unroll=u)))
@@ -47,6 +47,7 @@ def main():
     def setv(cfg):
         for k in ("row_variant", "resident_threads", "stream_threads", "stream_unroll"):
             _lib.set_tuning(k, cfg.get(k, 0))
+        _lib.set_tuning("resident_lb512", cfg.get("resident_lb512", 1))
 
     # copy / read reference points (torch's own kernels)
     ref = {}

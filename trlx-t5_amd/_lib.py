@@ -51,6 +51,15 @@ SIGNATURES = {
                                     _c_vp]),
     "trlx_ppo_loss_finalize": (_c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_d, _c_f, _c_vp, _c_vp, _c_vp]),
     "trlx_scale_by": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
+    "trlx_ppo_workspace_bytes": (_c_i64, [_c_i64, _c_i64]),
+    "trlx_ppo_experience_fused": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
+                                           _c_vp, _c_i64, _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_f,
+                                           _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,
+                                           _c_vp, _c_vp]),
+    "trlx_ppo_loss_fused": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
+                                     _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
+                                     _c_vp, _c_int, _c_vp, _c_int, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_i64,
+                                     _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
 }
 
 _lib = None

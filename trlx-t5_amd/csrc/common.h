@@ -250,6 +250,16 @@ struct RowSplit {
 // the row's VGPR footprint); unpacking again is 1-2 VALU ops per pair.
 __device__ __forceinline__ void launder(vec4u& v) { asm volatile("" : "+v"(v)); }
 
+// Buffer resources (T8): a wave-uniform 128-bit descriptor in SGPRs + a 32-bit per-lane
+// offset replaces a 64-bit address per 16-B vector (VGPR savings for register-resident
+// rows), and the hardware range check turns out-of-row lanes into no-ops (loads read 0,
+// stores are dropped).
+constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw buffer, dword3
+constexpr int kAuxNT = 2;               // nt cache policy (streamed, read/written once)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, int(bytes), kRsrcFlags);
+}
+
 // Streaming (read-once) 16-B load.
 __device__ __forceinline__ vec4u ld_stream(const vec4u* p) {
     return __builtin_nontemporal_load(p);

@@ -40,13 +40,17 @@ __device__ __forceinline__ float ppo_policy_dlp(float lp, float olp, float A, fl
 
 // mean and rsqrt(var + 1e-8) from a {sum, sumsq, count} fp64 record (modeling.py:24-34):
 // var = M2/count in the distributed branch, M2/(count-1) for torch.var_mean.
+// No fp64 division (its v_div_scale/v_rcp sequence would set the fused row kernel's
+// register peak): mean is an fp32 division, and M2 = Σx² − 2·m·Σx + n·m² with m = the
+// fp32 mean is exact up to n·(μ − m)² (~1e-14 relative), evaluated with fp64 fmas.
 __device__ __forceinline__ void whiten_coeffs(const double* st, int unbiased, float& mu, float& rstd) {
-    const double cnt = st[2];
-    const double mean = st[0] / cnt;
-    double m2 = st[1] - st[0] * mean;
+    const double sum = st[0], sumsq = st[1], cnt = st[2];
+    const float nf = float(cnt);
+    mu = float(sum) / nf;
+    const double m = double(mu);
+    double m2 = fma(m * cnt, m, fma(-2.0 * m, sum, sumsq));
     if (m2 < 0) m2 = 0;
-    mu = float(mean);
-    rstd = rsqrtf(float(m2 / (unbiased ? cnt - 1.0 : cnt)) + 1e-8f);
+    rstd = rsqrtf(float(m2) / (unbiased ? nf - 1.0f : nf) + 1e-8f);
 }
 
 }  // namespace trlx

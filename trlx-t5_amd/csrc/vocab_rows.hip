@@ -1,16 +1,18 @@
 // Vocab-axis row kernels: fused log-softmax + gather (forward), its backward, and the
-// loss-side fused forward+backward (logprob -> PPO policy gradient -> dlogits).
+// loss-side fused forward+backward (logprob -> PPO policy gradient -> dlogits), with the
+// rollout-level [T]-vector work (GAE, loss sums) folded into their tails (row_tails.h).
 //
-// One workgroup owns one logits row (b, t) of V elements.  The row is loaded ONCE from
-// HBM into registers as 16-byte vectors (NV per thread, all loads issued up front), the
-// max and sum-exp are wavefront-shuffle + LDS block reductions, and the backward /
-// fused kernels write dlogits from the same registers: 1 read (+1 write) of V*s bytes per
-// token, never materialising the [B,T,V] log-softmax the reference builds
-// (trlx/utils/modeling.py:39).  No MFMA: there is no contraction on this path; the
-// roofline is HBM bandwidth.
+// One workgroup owns one logits row (b, t) of V elements.  Register-resident variant: the
+// row is loaded ONCE from HBM into VGPRs as 16-byte buffer loads (NV per thread, all in
+// flight up front), max and sum-exp are wavefront-shuffle + LDS block reductions, and the
+// backward / fused kernels write dlogits from the same registers: 1 read (+1 write) of
+// V*s bytes per token, never materialising the [B,T,V] log-softmax the reference builds
+// (trlx/utils/modeling.py:39).  Streaming variant: online (max, sum-exp) over U vectors
+// in flight per thread, for rows too long to hold.  No MFMA: nothing here is a
+// contraction; the roofline is HBM bandwidth.
 #include <string>
 
-#include "ppo_math.h"
+#include "row_tails.h"
 
 namespace trlx {
 
@@ -46,154 +48,226 @@ struct RowArgs {
     // gradient output (bwd / ppo)
     void* dx;
     int64_t dsb, dst;
+    // rollout tails (fused experience / fused loss launches)
+    int tail;
+    Workspace ws;
+    ExpTailArgs exp;
+    LossTailArgs lt_;
 };
 
-template <class DT, int NV, int MODE>
-__global__ __launch_bounds__(kMaxThreads) void k_vocab_rows(RowArgs a) {
+// ------------------------------------------------------------------ shared row pieces
+template <class DT>
+struct Row {
+    typedef typename DT::elem_t E;
+    int64_t row, b, t;
+    const E* x;
+    int64_t y;
+    bool y_ok;
+    RowSplit<DT> s;
+    __device__ __forceinline__ Row(const RowArgs& a)
+        : row(blockIdx.x),
+          b(int64_t(blockIdx.x) / a.T),
+          t(int64_t(blockIdx.x) - (int64_t(blockIdx.x) / a.T) * a.T),
+          x(reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st),
+          y(a.labels[b * a.lb + t * a.lt]),
+          y_ok(y >= 0 && y < a.V),
+          s(x, a.V) {}
+    // head element -> threads [0, head); tail element -> the last `tail` threads
+    __device__ __forceinline__ int64_t edge_index() const {
+        const int tid = threadIdx.x, nthr = blockDim.x;
+        if (tid < s.head) return tid;
+        if (tid >= nthr - s.tail) return s.tail0 + (tid - (nthr - s.tail));
+        return -1;
+    }
+};
+
+// Row-independent per-token scalars of the fused PPO mode.
+struct PpoScalars {
+    float A, m, inv_msum, olp;
+};
+__device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row) {
+    PpoScalars p;
+    p.A = a.adv[row];
+    if (a.stats) {
+        float mu, rstd;
+        whiten_coeffs(a.stats, a.unbiased, mu, rstd);
+        p.A = mul_rn(p.A - mu, rstd);
+    }
+    p.m = a.mask ? float(a.mask[row]) : 1.0f;
+    const double msum = a.msum ? *a.msum : a.msum_host;
+    p.inv_msum = 1.0f / float(msum);  // torch: grad / mask.sum()
+    p.olp = ld_any(a.old_lp, a.old_dtype, row);
+    return p;
+}
+
+// Forward epilogue: write lp (+lse); with the experience tail, the workgroup completing a
+// rollout's 2T rows (policy + reference) runs its GAE.  All threads must call it.
+template <class DT>
+__device__ __forceinline__ void fwd_epilogue(const RowArgs& a, const Row<DT>& r, float lse) {
+    __shared__ int s_last;
+    const float lp = (r.y_ok ? DT::load1(r.x, r.y) : NAN) - lse;
+    if (!a.tail) {
+        if (threadIdx.x == 0) {
+            st_any(blockIdx.y == 0 ? a.lp0 : a.lp1, a.out_dtype, r.row, lp);
+            float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
+            if (lse_out) lse_out[r.row] = lse;
+        }
+        return;
+    }
+    if (threadIdx.x == 0) {
+        st_sc1(reinterpret_cast<float*>(blockIdx.y == 0 ? a.lp0 : a.lp1) + r.row, lp);
+        s_last = arrive_last(a.ws.row_ticket + r.b, unsigned(2 * a.T));
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < kWave)
+        experience_tail_row(a.exp, a.ws, int(r.b), int(a.T), reinterpret_cast<const float*>(a.lp0),
+                            reinterpret_cast<const float*>(a.lp1), int(a.B));
+}
+
+// Fused-loss epilogue after the row's dlogits are stored: the workgroup completing a
+// rollout's T rows sums its token records.  All threads must call it.
+__device__ __forceinline__ void ppo_epilogue(const RowArgs& a, int64_t b) {
+    __shared__ int s_last;
+    if (!a.tail) return;
+    if (threadIdx.x == 0) s_last = arrive_last(a.ws.row_ticket2 + b, unsigned(a.T));
+    __syncthreads();
+    if (s_last && threadIdx.x < kWave) {
+        const double msum = a.msum ? *a.msum : a.msum_host;
+        loss_tail_row(a.lt_, a.ws, int(b), int(a.T), int(a.B), msum);
+    }
+}
+
+// Per-token gradient scale g = d loss / d lp.
+template <int MODE>
+__device__ __forceinline__ float row_grad(const RowArgs& a, int64_t row, float lp, const PpoScalars& ps,
+                                          PolicyTerms& pt) {
+    if (MODE == kBwd) return ld_any(a.grad, a.grad_dtype, row);
+    const float g = ppo_policy_dlp(lp, ps.olp, ps.A, ps.m, ps.inv_msum, a.cliprange, pt);
+    if (threadIdx.x == 0) a.lp_out[row] = lp;
+    return g;
+}
+
+// After the row is stored (its registers dead): the token's loss record (fused loss).
+__device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, const PolicyTerms& pt,
+                                             const PpoScalars& ps) {
+    if (a.tail && threadIdx.x == 0) loss_token_terms(a.lt_, a.ws, row, 0.0f, pt, ps.m, ps.inv_msum);
+}
+
+// ------------------------------------------------------------------ register-resident rows
+// SAME_PHASE: every dlogits row starts at the same address mod 16 as its logits row (the
+// host checks strides and base phases; grad_buffer_like guarantees it), so dlogits are
+// written with the same aligned 16-B vectors.  The other instantiation writes elements.
+// LB512: launched with <= 512 threads, compiled for 6 waves per SIMD (opt-in knob).
+template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512>
+__global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vocab_rows(RowArgs a) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     typedef typename DT::elem_t E;
     constexpr int EPV = DT::kEPV;
-
-    const int64_t row = blockIdx.x;
-    const int64_t b = row / a.T, t = row - (row / a.T) * a.T;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    const E* xrow = reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st;
-    const int64_t y = a.labels[b * a.lb + t * a.lt];
-    const bool y_ok = (y >= 0) && (y < a.V);
+    const Row<DT> r(a);
+    // Row-independent scalars first: their arithmetic then runs before the row occupies
+    // its VGPRs.
+    PpoScalars ps = {0.f, 1.f, 1.f, 0.f};
+    if (MODE == kPpo) ps = ppo_scalars(a, r.row);
 
-    const RowSplit<DT> s(xrow, a.V);
-    const vec4u* vp = reinterpret_cast<const vec4u*>(xrow + s.head);
-
-    // ---- one HBM read of the row into registers (all loads in flight at once)
+    const int nvec = int(r.s.nvec);
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(r.x + r.s.head, uint32_t(nvec) * 16u);
+    const int voff = tid * 16;
+    // ---- one HBM read of the row into registers (all loads in flight at once).  Vectors
+    // past the row body read 0 (range check) and are excluded per vector below.
     vec4u v[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        const int64_t i = tid + int64_t(k) * nthr;
-        v[k] = (i < s.nvec) ? ld_stream(vp + i) : DT::neg_inf();
-    }
-    // head elements -> threads [0, head); tail elements -> the last `tail` threads
-    float ex = -INFINITY;
-    if (tid < s.head)
-        ex = DT::load1(xrow, tid);
-    else if (tid >= nthr - s.tail)
-        ex = DT::load1(xrow, s.tail0 + (tid - (nthr - s.tail)));
-    const float xy = y_ok ? DT::load1(xrow, y) : NAN;
+    for (int k = 0; k < NV; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, k * nthr * 16, kAuxNT);
+    const int64_t je = r.edge_index();
+    const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
 
-    float lse, lse_l2e;
+    float lse;
     if (MODE == kBwd) {
-        lse = a.lse_in[row];
+        lse = a.lse_in[r.row];
     } else {
-        // ---- row max
         float m = ex;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             float f[EPV];
             DT::unpack(v[k], f);
+            float mk = f[0];
 #pragma unroll
-            for (int e = 0; e < EPV; ++e) m = fmaxf(m, f[e]);
+            for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
+            m = (tid + k * nthr < nvec) ? fmaxf(m, mk) : m;
         }
         m = block_max(m, sh_max);
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
-        // ---- sum of exp(x - max)
         const float ml2e = -m * kLog2e;
         float sum = exp2_fast(fmaf(ex, kLog2e, ml2e));
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             float f[EPV];
             DT::unpack(v[k], f);
+            float sk = 0.0f;
 #pragma unroll
-            for (int e = 0; e < EPV; ++e) sum += exp2_fast(fmaf(f[e], kLog2e, ml2e));
+            for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
+            sum += (tid + k * nthr < nvec) ? sk : 0.0f;
         }
         sum = block_sum(sum, sh_sum);
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
         lse = m + logf(sum);
     }
-    const float lp = xy - lse;
-
     if (MODE == kFwd) {
-        if (tid == 0) {
-            void* out = blockIdx.y == 0 ? a.lp0 : a.lp1;
-            float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
-            st_any(out, a.out_dtype, row, lp);
-            if (lse_out) lse_out[row] = lse;
-        }
+        fwd_epilogue(a, r, lse);
         return;
     }
-
-    // ---- per-row gradient scale g = d loss / d lp
-    float g;
-    if (MODE == kBwd) {
-        g = ld_any(a.grad, a.grad_dtype, row);
-    } else {
-        float A = a.adv[row];
-        if (a.stats) {
-            float mu, rstd;
-            whiten_coeffs(a.stats, a.unbiased, mu, rstd);
-            A = mul_rn(A - mu, rstd);
-        }
-        const float mval = a.mask ? float(a.mask[row]) : 1.0f;
-        const double msum = a.msum ? *a.msum : a.msum_host;
-        const float inv_msum = 1.0f / float(msum);  // torch: grad / mask.sum()
-        const float olp = ld_any(a.old_lp, a.old_dtype, row);
-        PolicyTerms pt;
-        g = ppo_policy_dlp(lp, olp, A, mval, inv_msum, a.cliprange, pt);
-        if (tid == 0) a.lp_out[row] = lp;
-    }
+    const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
+    PolicyTerms pt = {1.f, 0.f, 0.f, false};
+    const float g = row_grad<MODE>(a, r.row, xy - lse, ps, pt);
 
     // ---- dlogits = g * (onehot(y) - exp(x - lse)), written once
-    lse_l2e = -lse * kLog2e;
-    E* drow = reinterpret_cast<E*>(a.dx) + b * a.dsb + t * a.dst;
+    const float lse_l2e = -lse * kLog2e;
+    E* drow = reinterpret_cast<E*>(a.dx) + r.b * a.dsb + r.t * a.dst;
     const float gy = g * (1.0f - exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
-    const bool same_phase = ((reinterpret_cast<uintptr_t>(drow) ^ reinterpret_cast<uintptr_t>(xrow)) & 15u) == 0;
-    if (same_phase) {
-        vec4u* dvp = reinterpret_cast<vec4u*>(drow + s.head);
-        const int64_t iy = y_ok && y >= s.head && y < s.tail0 ? (y - s.head) / EPV : -1;
+    if (SAME_PHASE) {
+        const __amdgpu_buffer_rsrc_t rout = make_rsrc(drow + r.s.head, uint32_t(nvec) * 16u);
+        const int iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? int((r.y - r.s.head) / EPV) : -1;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const int64_t i = tid + int64_t(k) * nthr;
-            if (i < s.nvec) {
-                float f[EPV];
-                DT::unpack(v[k], f);
+            const int i = tid + k * nthr;  // lanes past the body: the store is range-checked away
+            float f[EPV];
+            DT::unpack(v[k], f);
 #pragma unroll
-                for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
-                if (i == iy) {  // the label's vector: onehot term
-                    const int ey = int(y - (s.head + i * EPV));
+            for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+            if (i == iy) {  // the label's vector: onehot term
+                const int ey = int(r.y - (r.s.head + int64_t(i) * EPV));
 #pragma unroll
-                    for (int e = 0; e < EPV; ++e)
-                        if (e == ey) f[e] = gy;
-                }
-                __builtin_nontemporal_store(DT::pack(f), dvp + i);
+                for (int e = 0; e < EPV; ++e)
+                    if (e == ey) f[e] = gy;
             }
+            __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, voff, k * nthr * 16, kAuxNT);
         }
     } else {
-        // dlogits row not co-aligned with the logits row: element stores (correct, slower)
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const int64_t i = tid + int64_t(k) * nthr;
-            if (i < s.nvec) {
+            const int i = tid + k * nthr;
+            if (i < nvec) {
                 float f[EPV];
                 DT::unpack(v[k], f);
 #pragma unroll
                 for (int e = 0; e < EPV; ++e) {
-                    const int64_t j = s.head + i * EPV + e;
-                    DT::store1(drow, j, j == y ? gy : -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
+                    const int64_t j = r.s.head + int64_t(i) * EPV + e;
+                    DT::store1(drow, j, j == r.y ? gy : -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
                 }
             }
         }
     }
-    // head / tail elements
-    int64_t jx = -1;
-    if (tid < s.head)
-        jx = tid;
-    else if (tid >= nthr - s.tail)
-        jx = s.tail0 + (tid - (nthr - s.tail));
-    if (jx >= 0) DT::store1(drow, jx, jx == y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+    if (MODE == kPpo) {
+        token_record(a, r.row, pt, ps);
+        ppo_epilogue(a, r.b);
+    }
 }
 
-// ------------------------------------------------------------------ streaming variant
+// ------------------------------------------------------------------ streaming rows
 // Same arithmetic, but the row is streamed through registers U vectors at a time with an
 // online (max, sum-exp) instead of being held whole: small register footprint => many
 // workgroups per CU keep loads continuously in flight.  Backward / fused modes make a
@@ -213,32 +287,26 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
     __shared__ float sh_s[kStreamMaxThreads / kWave];
     typedef typename DT::elem_t E;
     constexpr int EPV = DT::kEPV;
-    const int64_t row = blockIdx.x;
-    const int64_t b = row / a.T, t = row - (row / a.T) * a.T;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    const E* xrow = reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st;
-    const int64_t y = a.labels[b * a.lb + t * a.lt];
-    const bool y_ok = (y >= 0) && (y < a.V);
-    const RowSplit<DT> s(xrow, a.V);
-    const vec4u* vp = reinterpret_cast<const vec4u*>(xrow + s.head);
-    float ex = -INFINITY;
-    if (tid < s.head)
-        ex = DT::load1(xrow, tid);
-    else if (tid >= nthr - s.tail)
-        ex = DT::load1(xrow, s.tail0 + (tid - (nthr - s.tail)));
-    const float xy = y_ok ? DT::load1(xrow, y) : NAN;
+    const Row<DT> r(a);
+    PpoScalars ps = {0.f, 1.f, 1.f, 0.f};
+    if (MODE == kPpo) ps = ppo_scalars(a, r.row);
+    const vec4u* vp = reinterpret_cast<const vec4u*>(r.x + r.s.head);
+    const int64_t nvec = r.s.nvec;
+    const int64_t je = r.edge_index();
+    const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
 
     float lse;
     if (MODE == kBwd) {
-        lse = a.lse_in[row];
+        lse = a.lse_in[r.row];
     } else {
         float m = ex, sum = (ex == -INFINITY) ? 0.0f : 1.0f;
-        for (int64_t base = tid; base < s.nvec; base += int64_t(nthr) * U) {
+        for (int64_t base = tid; base < nvec; base += int64_t(nthr) * U) {
             vec4u v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t i = base + int64_t(u) * nthr;
-                v[u] = (i < s.nvec) ? ld_stream(vp + i) : DT::neg_inf();
+                v[u] = (i < nvec) ? ld_stream(vp + i) : DT::neg_inf();
             }
             float mx = -INFINITY;
 #pragma unroll
@@ -263,7 +331,6 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
             }
             m = nm;
         }
-        // wave combine, then fixed-order cross-wave combine
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const float m2 = __shfl_xor(m, off, kWave), s2 = __shfl_xor(sum, off, kWave);
@@ -279,58 +346,37 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
         for (int w = 1; w < nthr / kWave; ++w) online_merge(m, sum, sh_m[w], sh_s[w]);
         lse = m + logf(sum);
     }
-    const float lp = xy - lse;
     if (MODE == kFwd) {
-        if (tid == 0) {
-            void* out = blockIdx.y == 0 ? a.lp0 : a.lp1;
-            float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
-            st_any(out, a.out_dtype, row, lp);
-            if (lse_out) lse_out[row] = lse;
-        }
+        fwd_epilogue(a, r, lse);
         return;
     }
-    float g;
-    if (MODE == kBwd) {
-        g = ld_any(a.grad, a.grad_dtype, row);
-    } else {
-        float A = a.adv[row];
-        if (a.stats) {
-            float mu, rstd;
-            whiten_coeffs(a.stats, a.unbiased, mu, rstd);
-            A = mul_rn(A - mu, rstd);
-        }
-        const float mval = a.mask ? float(a.mask[row]) : 1.0f;
-        const double msum = a.msum ? *a.msum : a.msum_host;
-        const float inv_msum = 1.0f / float(msum);
-        const float olp = ld_any(a.old_lp, a.old_dtype, row);
-        PolicyTerms pt;
-        g = ppo_policy_dlp(lp, olp, A, mval, inv_msum, a.cliprange, pt);
-        if (tid == 0) a.lp_out[row] = lp;
-    }
+    const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
+    PolicyTerms pt = {1.f, 0.f, 0.f, false};
+    const float g = row_grad<MODE>(a, r.row, xy - lse, ps, pt);
     const float lse_l2e = -lse * kLog2e;
-    E* drow = reinterpret_cast<E*>(a.dx) + b * a.dsb + t * a.dst;
+    E* drow = reinterpret_cast<E*>(a.dx) + r.b * a.dsb + r.t * a.dst;
     const float gy = g * (1.0f - exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
-    const bool same_phase = ((reinterpret_cast<uintptr_t>(drow) ^ reinterpret_cast<uintptr_t>(xrow)) & 15u) == 0;
-    const int64_t iy = y_ok && y >= s.head && y < s.tail0 ? (y - s.head) / EPV : -1;
-    vec4u* dvp = reinterpret_cast<vec4u*>(drow + s.head);
-    for (int64_t base = tid; base < s.nvec; base += int64_t(nthr) * U) {
+    const bool same_phase = ((reinterpret_cast<uintptr_t>(drow) ^ reinterpret_cast<uintptr_t>(r.x)) & 15u) == 0;
+    const int64_t iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? (r.y - r.s.head) / EPV : -1;
+    vec4u* dvp = reinterpret_cast<vec4u*>(drow + r.s.head);
+    for (int64_t base = tid; base < nvec; base += int64_t(nthr) * U) {
         vec4u v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t i = base + int64_t(u) * nthr;
-            if (i < s.nvec) v[u] = vp[i];  // second touch: cached read
+            if (i < nvec) v[u] = vp[i];  // second touch: cached read
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t i = base + int64_t(u) * nthr;
-            if (i >= s.nvec) continue;
+            if (i >= nvec) continue;
             float f[EPV];
             DT::unpack(v[u], f);
 #pragma unroll
             for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
             if (same_phase) {
                 if (i == iy) {
-                    const int ey = int(y - (s.head + i * EPV));
+                    const int ey = int(r.y - (r.s.head + i * EPV));
 #pragma unroll
                     for (int e = 0; e < EPV; ++e)
                         if (e == ey) f[e] = gy;
@@ -339,33 +385,37 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
             } else {
 #pragma unroll
                 for (int e = 0; e < EPV; ++e) {
-                    const int64_t j = s.head + i * EPV + e;
-                    DT::store1(drow, j, j == y ? gy : f[e]);
+                    const int64_t j = r.s.head + i * EPV + e;
+                    DT::store1(drow, j, j == r.y ? gy : f[e]);
                 }
             }
         }
     }
-    int64_t jx = -1;
-    if (tid < s.head)
-        jx = tid;
-    else if (tid >= nthr - s.tail)
-        jx = s.tail0 + (tid - (nthr - s.tail));
-    if (jx >= 0) DT::store1(drow, jx, jx == y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+    if (MODE == kPpo) {
+        token_record(a, r.row, pt, ps);
+        ppo_epilogue(a, r.b);
+    }
 }
 
 // ------------------------------------------------------------------ launch geometry
-// Vectors per thread (NV) are compile-time so the row lives in registers; threads per
-// block = the smallest multiple of 64 that covers the row with NV vectors.
 struct Geometry {
     int nv;
     int threads;
 };
-static int g_resident_threads = 0;  // preferred workgroup size for resident rows (0 = auto)
+
+// Tuning knobs (trlx_set_tuning): 0 = automatic.
+static int g_row_variant = 0;       // 1 = register-resident rows, 2 = streaming rows
+static int g_resident_threads = 0;  // preferred workgroup size for resident rows
+static int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 6 waves/SIMD
+static int g_stream_threads = 0;
+static int g_stream_unroll = 0;
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
 // workgroup size.  Default: 512-thread workgroups (8 waves) -- measured on MI355X (C2,
-// bf16 V=50257) to keep 3 rows in flight per CU at ~71 VGPRs, 6.7 TB/s for the forward;
-// rows too long for 16 vectors x 512 threads use 1024 threads, then the streaming kernel.
+// bf16 V=50257): 3 rows in flight per CU at ~71 VGPRs, 6.6-6.7 TB/s for the forward;
+// rows too long for 16 vectors x 512 threads use 1024 threads (backward / fused) or the
+// streaming kernel (forward: measured faster than 1024-thread resident rows).
 static const int kNVs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 16};
 
 static Geometry pick_geometry(int64_t V, int elem_bytes, bool allow_1024) {
@@ -386,17 +436,17 @@ static Geometry pick_geometry(int64_t V, int elem_bytes, bool allow_1024) {
     return {0, 0};
 }
 
-// Tuning knobs (trlx_set_tuning): 0 = automatic.
-static int g_row_variant = 0;   // 1 = register-resident rows, 2 = streaming rows
-static int g_stream_threads = 0;
-static int g_stream_unroll = 0;
+// True when every dlogits row (b, t) has the same 16-byte phase as its logits row.
+static bool rows_same_phase(const RowArgs& a, size_t es) {
+    if (!a.dx) return true;
+    const bool same_steps = (a.B <= 1 || ((a.sb - a.dsb) * int64_t(es)) % 16 == 0) &&
+                            (a.T <= 1 || ((a.st - a.dst) * int64_t(es)) % 16 == 0);
+    return same_steps && ((reinterpret_cast<uintptr_t>(a.x0) ^ reinterpret_cast<uintptr_t>(a.dx)) & 15u) == 0;
+}
 
 template <int MODE, class DT>
 static int launch_rows_dt(const RowArgs& a, int nten, hipStream_t stream) {
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
-    // Forward (read-only): resident rows while a 512-thread workgroup holds the row, else
-    // streaming (measured: 1024-thread resident rows lose ~20% to streaming on fp32 V=50257).
-    // Backward / fused (read + write): resident up to 1024 threads (one read instead of two).
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
     if (variant == 2 || g.nv == 0) {
@@ -411,8 +461,17 @@ static int launch_rows_dt(const RowArgs& a, int nten, hipStream_t stream) {
         return check_launch("k_vocab_rows_stream");
     }
     const dim3 block(g.threads);
-#define TRLX_RESIDENT_CASE(N) \
-    case N: hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE>), grid, block, 0, stream, a); break;
+    const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
+    const bool lb512 = g.threads <= 512 && g_resident_lb512;
+#define TRLX_RESIDENT_CASE(N)                                                                          \
+    case N:                                                                                           \
+        if (same && lb512)                                                                            \
+            hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE, true, true>), grid, block, 0, stream, a);   \
+        else if (same)                                                                                \
+            hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE, true, false>), grid, block, 0, stream, a);  \
+        else                                                                                          \
+            hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE, MODE == kFwd, false>), grid, block, 0, stream, a); \
+        break;
     switch (g.nv) {
         TRLX_RESIDENT_CASE(1) TRLX_RESIDENT_CASE(2) TRLX_RESIDENT_CASE(3) TRLX_RESIDENT_CASE(4)
         TRLX_RESIDENT_CASE(5) TRLX_RESIDENT_CASE(6) TRLX_RESIDENT_CASE(7) TRLX_RESIDENT_CASE(8)
@@ -435,8 +494,34 @@ static int check_rows(const RowArgs& a, int dtype) {
     TRLX_REQUIRE(a.B >= 0 && a.T >= 0 && a.V > 0, TRLX_ERR_SHAPE, "bad shape B=%lld T=%lld V=%lld",
                  (long long)a.B, (long long)a.T, (long long)a.V);
     TRLX_REQUIRE(a.B * a.T <= 0x7fffffffLL, TRLX_ERR_SHAPE, "too many rows");
+    TRLX_REQUIRE(a.V * 16 < (1LL << 32), TRLX_ERR_SHAPE, "vocab too large");
     TRLX_REQUIRE(a.x0 && a.labels, TRLX_ERR_ARG, "NULL logits/labels");
     return TRLX_OK;
+}
+
+// Workspace carve-up (all sections 16-B aligned), shared by both fused launches.
+static size_t ws_align(size_t x) { return (x + 15) & ~size_t(15); }
+static size_t carve_workspace(void* base, int64_t B, int64_t T, Workspace* w) {
+    char* p = static_cast<char*>(base);
+    size_t off = 0;
+    const size_t tick = ws_align(sizeof(unsigned) * size_t(B + 1));
+    if (w) {
+        w->row_ticket = reinterpret_cast<unsigned*>(p + off);
+        w->all_ticket = w->row_ticket + B;
+    }
+    off += tick;
+    if (w) {
+        w->row_ticket2 = reinterpret_cast<unsigned*>(p + off);
+        w->all_ticket2 = w->row_ticket2 + B;
+    }
+    off += tick;
+    if (w) w->mom = reinterpret_cast<double*>(p + off);
+    off += ws_align(sizeof(double) * 4 * size_t(B));
+    if (w) w->rowrec = reinterpret_cast<double*>(p + off);
+    off += ws_align(sizeof(double) * 16 * size_t(B));
+    if (w) w->tokrec = reinterpret_cast<float*>(p + off);
+    off += ws_align(sizeof(float) * kTokRec * size_t(B * T));
+    return off;
 }
 
 }  // namespace trlx
@@ -466,7 +551,7 @@ extern "C" int trlx_lsm_gather_bwd(const void* x, int dtype, int64_t B, int64_t 
     RowArgs a = {};
     a.x0 = x; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
     a.lse_in = lse; a.grad = grad; a.grad_dtype = grad_dtype; a.dx = dx; a.dsb = dsb; a.dst = dst;
-    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;  // empty batch: nothing to launch
+    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;
     int rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(lse && grad && dx, TRLX_ERR_ARG, "NULL lse/grad/dx");
@@ -484,7 +569,7 @@ extern "C" int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_
     a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv; a.stats = stats; a.unbiased = unbiased;
     a.mask = mask; a.msum = msum; a.msum_host = msum_host; a.cliprange = cliprange;
     a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
-    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;  // empty batch: nothing to launch
+    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;
     int rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(old_lp && adv && lp_out && dx, TRLX_ERR_ARG, "NULL old_lp/adv/lp_out/dx");
@@ -492,23 +577,78 @@ extern "C" int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_
     return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
 }
 
+extern "C" int64_t trlx_ppo_workspace_bytes(int64_t B, int64_t T) {
+    return int64_t(carve_workspace(nullptr, B, T, nullptr));
+}
+
+extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dtype, int64_t B,
+                                         int64_t T, int64_t V, int64_t sb, int64_t st, const int64_t* labels,
+                                         int64_t lb, int64_t lt, const void* values, int v_dtype,
+                                         const float* scores, const int64_t* lengths, const int64_t* mask,
+                                         float kl_coef, float gamma, float lam, float* lp, float* ref_lp,
+                                         float* rewards, float* adv_raw, void* ret, int ret_dtype,
+                                         double* stats, void* workspace, void* stream) {
+    RowArgs a = {};
+    a.x0 = logits; a.x1 = ref_logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
+    a.labels = labels; a.lb = lb; a.lt = lt; a.lp0 = lp; a.lp1 = ref_lp; a.out_dtype = TRLX_F32;
+    int rc = check_rows(a, dtype);
+    if (rc) return rc;
+    TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
+    TRLX_REQUIRE(ref_logits && values && lp && ref_lp && rewards && adv_raw && ret && stats && workspace,
+                 TRLX_ERR_ARG, "NULL argument to trlx_ppo_experience_fused");
+    a.tail = 1;
+    carve_workspace(workspace, B, T, &a.ws);
+    a.exp.values = values; a.exp.v_dtype = v_dtype; a.exp.scores = scores; a.exp.lengths = lengths;
+    a.exp.mask = mask; a.exp.neg_beta = -kl_coef; a.exp.gamma = gamma;
+    a.exp.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
+    a.exp.rewards = rewards; a.exp.adv = adv_raw; a.exp.ret = ret; a.exp.ret_dtype = ret_dtype;
+    a.exp.stats = stats;
+    return launch_rows<kFwd>(a, dtype, 2, (hipStream_t)stream);
+}
+
+extern "C" int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
+                                   int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
+                                   int old_dtype, const float* adv_raw, const double* stats, int unbiased,
+                                   const int64_t* mask, const void* values, int v_dtype, const void* old_values,
+                                   int ov_dtype, const void* returns, int r_dtype, float cliprange,
+                                   float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb,
+                                   int64_t dst, float* dvalues, float* loss, float* loss_stats, void* workspace,
+                                   void* stream) {
+    RowArgs a = {};
+    a.x0 = logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
+    a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv_raw; a.stats = stats; a.unbiased = unbiased;
+    a.mask = mask; a.msum = stats ? stats + 3 : nullptr; a.msum_host = double(B * T); a.cliprange = cliprange;
+    a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
+    int rc = check_rows(a, dtype);
+    if (rc) return rc;
+    TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
+    TRLX_REQUIRE(old_lp && adv_raw && stats && values && old_values && returns && lp_out && dx && dvalues && loss &&
+                     loss_stats && workspace,
+                 TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_fused");
+    a.tail = 1;
+    carve_workspace(workspace, B, T, &a.ws);
+    a.lt_.values = values; a.lt_.v_dtype = v_dtype; a.lt_.old_values = old_values; a.lt_.ov_dtype = ov_dtype;
+    a.lt_.returns = returns; a.lt_.r_dtype = r_dtype; a.lt_.cv = cliprange_value; a.lt_.vf_coef = vf_coef;
+    a.lt_.dv = dvalues; a.lt_.loss = loss; a.lt_.stats = loss_stats;
+    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
+}
+
 extern "C" int trlx_set_tuning(const char* key, int64_t value) {
     const std::string k = key ? key : "";
     if (k == "row_variant") g_row_variant = int(value);
+    else if (k == "resident_lb512") g_resident_lb512 = int(value);
     else if (k == "resident_threads") {
         TRLX_REQUIRE(value == 0 || (value % kWave == 0 && value <= kMaxThreads), TRLX_ERR_ARG,
                      "resident_threads must be a multiple of 64 <= %d", kMaxThreads);
         g_resident_threads = int(value);
-    }
-    else if (k == "stream_threads") {
+    } else if (k == "stream_threads") {
         TRLX_REQUIRE(value == 0 || (value % kWave == 0 && value <= kStreamMaxThreads), TRLX_ERR_ARG,
                      "stream_threads must be a multiple of 64 <= %d", kStreamMaxThreads);
         g_stream_threads = int(value);
     } else if (k == "stream_unroll") {
         TRLX_REQUIRE(value == 0 || value == 2 || value == 4 || value == 8, TRLX_ERR_ARG, "stream_unroll: 2, 4 or 8");
         g_stream_unroll = int(value);
-    }
-    else {
+    } else {
         set_error("unknown tuning key '%s'", k.c_str());
         return TRLX_ERR_ARG;
     }
