@@ -249,6 +249,10 @@ struct RowSplit {
 // register-resident bf16 row alive across the max / sum / store passes (it would double
 // the row's VGPR footprint); unpacking again is 1-2 VALU ops per pair.
 __device__ __forceinline__ void launder(vec4u& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ int launder_int(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
 
 // Buffer resources (T8): a wave-uniform 128-bit descriptor in SGPRs + a 32-bit per-lane
 // offset replaces a 64-bit address per 16-B vector (VGPR savings for register-resident

@@ -38,24 +38,7 @@ __device__ void ppo_loss_emit(double tot, int64_t n, double msum, float vf_coef,
     if (threadIdx.x != 0) return;
     double acc[kSlots];
     for (int k = 0; k < kSlots; ++k) acc[k] = sh[k];
-    const double N = double(n);
-    const double vf = 0.5 * acc[0] / msum;
-    const double pg = acc[3] / msum;
-    const double total = pg + double(vf_coef) * vf;
-    loss[0] = float(total);
-    stats[0] = float(total);                                // losses/total_loss
-    stats[1] = float(pg);                                   // losses/policy_loss
-    stats[2] = float(vf);                                   // losses/value_loss
-    stats[3] = float(acc[5] / N);                           // values/mean_old_values
-    stats[4] = float((acc[6] - acc[5] * acc[5] / N) / (N - 1.0));  // values/var_old_values
-    stats[5] = float(acc[7] / N);                           // values/mean_values
-    stats[6] = float(acc[8] / N);                           // values/values_error
-    stats[7] = float(acc[1] / N);                           // values/clipfrac
-    stats[8] = float(acc[2] / N);                           // policy/approx_kl
-    stats[9] = float(acc[4] / N);                           // policy/clipfrac
-    stats[10] = float(acc[9] / N);                          // returns/mean
-    stats[11] = float((acc[10] - acc[9] * acc[9] / N) / (N - 1.0));  // returns/var
-    stats[12] = float(acc[11] / msum);                      // ratio
+    emit_loss_stats(acc, double(n), msum, vf_coef, loss, stats);
 }
 
 __global__ __launch_bounds__(kLossThreads) void k_ppo_loss_elem(LossArgs a) {

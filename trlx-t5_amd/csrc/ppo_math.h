@@ -53,4 +53,32 @@ __device__ __forceinline__ void whiten_coeffs(const double* st, int unbiased, fl
     rstd = rsqrtf(float(m2) / (unbiased ? nf - 1.0f : nf) + 1e-8f);
 }
 
+// Loss and the 13 stats of PPOConfig.loss (ppo_models.py:162-198) from fp64 sums:
+//   acc[0] Σ max(vl1,vl2)·m   acc[1] #(vl2 > vl1)   acc[2] Σ (ratio-1) - log_ratio
+//   acc[3] Σ max(pg1,pg2)·m   acc[4] #(pg2 > pg1)   acc[5] Σ old_values   acc[6] Σ old_values²
+//   acc[7] Σ values           acc[8] Σ (values-returns)²                  acc[9] Σ returns
+//   acc[10] Σ returns²        acc[11] Σ ratio·m     acc[12] Σ m
+// Divisions by N are torch.mean; var is torch.var (unbiased).
+constexpr int kLossSums = 13;
+__device__ __forceinline__ void emit_loss_stats(const double* acc, double N, double msum, float vf_coef,
+                                                float* loss, float* s) {
+    const double vf = 0.5 * acc[0] / msum;
+    const double pg = acc[3] / msum;
+    const double tot = pg + double(vf_coef) * vf;
+    loss[0] = float(tot);
+    s[0] = float(tot);                                         // losses/total_loss
+    s[1] = float(pg);                                          // losses/policy_loss
+    s[2] = float(vf);                                          // losses/value_loss
+    s[3] = float(acc[5] / N);                                  // values/mean_old_values
+    s[4] = float((acc[6] - acc[5] * acc[5] / N) / (N - 1.0));  // values/var_old_values
+    s[5] = float(acc[7] / N);                                  // values/mean_values
+    s[6] = float(acc[8] / N);                                  // values/values_error
+    s[7] = float(acc[1] / N);                                  // values/clipfrac
+    s[8] = float(acc[2] / N);                                  // policy/approx_kl
+    s[9] = float(acc[4] / N);                                  // policy/clipfrac
+    s[10] = float(acc[9] / N);                                 // returns/mean
+    s[11] = float((acc[10] - acc[9] * acc[9] / N) / (N - 1.0));  // returns/var
+    s[12] = float(acc[11] / msum);                             // ratio
+}
+
 }  // namespace trlx

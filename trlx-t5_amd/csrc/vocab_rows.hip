@@ -1,6 +1,6 @@
 // Vocab-axis row kernels: fused log-softmax + gather (forward), its backward, and the
-// loss-side fused forward+backward (logprob -> PPO policy gradient -> dlogits), with the
-// rollout-level [T]-vector work (GAE, loss sums) folded into their tails (row_tails.h).
+// loss-side fused forward+backward (logprob -> PPO policy gradient -> dlogits); the fused
+// step's rollout-level [T]-vector work runs in one-wave-per-rollout kernels (row_tails.h).
 //
 // One workgroup owns one logits row (b, t) of V elements.  Register-resident variant: the
 // row is loaded ONCE from HBM into VGPRs as 16-byte buffer loads (NV per thread, all in
@@ -48,11 +48,9 @@ struct RowArgs {
     // gradient output (bwd / ppo)
     void* dx;
     int64_t dsb, dst;
-    // rollout tails (fused experience / fused loss launches)
-    int tail;
-    Workspace ws;
-    ExpTailArgs exp;
-    LossTailArgs lt_;
+    // fused loss: per-token loss records + value gradient (row_tails.h)
+    float* tokrec;
+    LossTokenArgs ltok;
 };
 
 // ------------------------------------------------------------------ shared row pieces
@@ -100,40 +98,14 @@ __device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row)
     return p;
 }
 
-// Forward epilogue: write lp (+lse); with the experience tail, the workgroup completing a
-// rollout's 2T rows (policy + reference) runs its GAE.  All threads must call it.
+// Forward epilogue: write lp (+lse).
 template <class DT>
 __device__ __forceinline__ void fwd_epilogue(const RowArgs& a, const Row<DT>& r, float lse) {
-    __shared__ int s_last;
-    const float lp = (r.y_ok ? DT::load1(r.x, r.y) : NAN) - lse;
-    if (!a.tail) {
-        if (threadIdx.x == 0) {
-            st_any(blockIdx.y == 0 ? a.lp0 : a.lp1, a.out_dtype, r.row, lp);
-            float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
-            if (lse_out) lse_out[r.row] = lse;
-        }
-        return;
-    }
     if (threadIdx.x == 0) {
-        st_sc1(reinterpret_cast<float*>(blockIdx.y == 0 ? a.lp0 : a.lp1) + r.row, lp);
-        s_last = arrive_last(a.ws.row_ticket + r.b, unsigned(2 * a.T));
-    }
-    __syncthreads();
-    if (s_last && threadIdx.x < kWave)
-        experience_tail_row(a.exp, a.ws, int(r.b), int(a.T), reinterpret_cast<const float*>(a.lp0),
-                            reinterpret_cast<const float*>(a.lp1), int(a.B));
-}
-
-// Fused-loss epilogue after the row's dlogits are stored: the workgroup completing a
-// rollout's T rows sums its token records.  All threads must call it.
-__device__ __forceinline__ void ppo_epilogue(const RowArgs& a, int64_t b) {
-    __shared__ int s_last;
-    if (!a.tail) return;
-    if (threadIdx.x == 0) s_last = arrive_last(a.ws.row_ticket2 + b, unsigned(a.T));
-    __syncthreads();
-    if (s_last && threadIdx.x < kWave) {
-        const double msum = a.msum ? *a.msum : a.msum_host;
-        loss_tail_row(a.lt_, a.ws, int(b), int(a.T), int(a.B), msum);
+        const float lp = (r.y_ok ? DT::load1(r.x, r.y) : NAN) - lse;
+        st_any(blockIdx.y == 0 ? a.lp0 : a.lp1, a.out_dtype, r.row, lp);
+        float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
+        if (lse_out) lse_out[r.row] = lse;
     }
 }
 
@@ -150,7 +122,7 @@ __device__ __forceinline__ float row_grad(const RowArgs& a, int64_t row, float l
 // After the row is stored (its registers dead): the token's loss record (fused loss).
 __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, const PolicyTerms& pt,
                                              const PpoScalars& ps) {
-    if (a.tail && threadIdx.x == 0) loss_token_terms(a.lt_, a.ws, row, 0.0f, pt, ps.m, ps.inv_msum);
+    if (a.tokrec && threadIdx.x == 0) loss_token_terms(a.ltok, a.tokrec, row, pt, ps.m, ps.inv_msum);
 }
 
 // ------------------------------------------------------------------ register-resident rows
@@ -173,12 +145,14 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
 
     const int nvec = int(r.s.nvec);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(r.x + r.s.head, uint32_t(nvec) * 16u);
-    const int voff = tid * 16;
+    const int voff = tid * 16;  // + k*nthr*16 per vector, in VOFFSET: the raw-buffer range
+                                // check covers voffset (+imm), not soffset
     // ---- one HBM read of the row into registers (all loads in flight at once).  Vectors
     // past the row body read 0 (range check) and are excluded per vector below.
     vec4u v[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, k * nthr * 16, kAuxNT);
+    for (int k = 0; k < NV; ++k)
+        v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, launder_int(voff) + k * nthr * 16, 0, kAuxNT);
     const int64_t je = r.edge_index();
     const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
 
@@ -243,7 +217,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
                 for (int e = 0; e < EPV; ++e)
                     if (e == ey) f[e] = gy;
             }
-            __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, voff, k * nthr * 16, kAuxNT);
+            __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, launder_int(voff) + k * nthr * 16, 0, kAuxNT);
         }
     } else {
 #pragma unroll
@@ -261,10 +235,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
         }
     }
     if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
-    if (MODE == kPpo) {
-        token_record(a, r.row, pt, ps);
-        ppo_epilogue(a, r.b);
-    }
+    if (MODE == kPpo) token_record(a, r.row, pt, ps);
 }
 
 // ------------------------------------------------------------------ streaming rows
@@ -392,10 +363,7 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
         }
     }
     if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
-    if (MODE == kPpo) {
-        token_record(a, r.row, pt, ps);
-        ppo_epilogue(a, r.b);
-    }
+    if (MODE == kPpo) token_record(a, r.row, pt, ps);
 }
 
 // ------------------------------------------------------------------ launch geometry
@@ -499,26 +467,18 @@ static int check_rows(const RowArgs& a, int dtype) {
     return TRLX_OK;
 }
 
-// Workspace carve-up (all sections 16-B aligned), shared by both fused launches.
+// Workspace carve-up (16-B aligned sections), shared by both fused launches.
 static size_t ws_align(size_t x) { return (x + 15) & ~size_t(15); }
 static size_t carve_workspace(void* base, int64_t B, int64_t T, Workspace* w) {
     char* p = static_cast<char*>(base);
+    const int64_t nblk = (B + kRolloutsPerBlock - 1) / kRolloutsPerBlock;
     size_t off = 0;
-    const size_t tick = ws_align(sizeof(unsigned) * size_t(B + 1));
-    if (w) {
-        w->row_ticket = reinterpret_cast<unsigned*>(p + off);
-        w->all_ticket = w->row_ticket + B;
-    }
-    off += tick;
-    if (w) {
-        w->row_ticket2 = reinterpret_cast<unsigned*>(p + off);
-        w->all_ticket2 = w->row_ticket2 + B;
-    }
-    off += tick;
-    if (w) w->mom = reinterpret_cast<double*>(p + off);
-    off += ws_align(sizeof(double) * 4 * size_t(B));
-    if (w) w->rowrec = reinterpret_cast<double*>(p + off);
-    off += ws_align(sizeof(double) * 16 * size_t(B));
+    if (w) w->tickets = reinterpret_cast<unsigned*>(p + off);
+    off += 16;
+    if (w) w->gae_rec = reinterpret_cast<double*>(p + off);
+    off += ws_align(sizeof(double) * TRLX_MOMENT_SLOTS * size_t(nblk));
+    if (w) w->loss_rec = reinterpret_cast<double*>(p + off);
+    off += ws_align(sizeof(double) * 16 * size_t(nblk));
     if (w) w->tokrec = reinterpret_cast<float*>(p + off);
     off += ws_align(sizeof(float) * kTokRec * size_t(B * T));
     return off;
@@ -596,14 +556,18 @@ extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_log
     TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
     TRLX_REQUIRE(ref_logits && values && lp && ref_lp && rewards && adv_raw && ret && stats && workspace,
                  TRLX_ERR_ARG, "NULL argument to trlx_ppo_experience_fused");
-    a.tail = 1;
-    carve_workspace(workspace, B, T, &a.ws);
-    a.exp.values = values; a.exp.v_dtype = v_dtype; a.exp.scores = scores; a.exp.lengths = lengths;
-    a.exp.mask = mask; a.exp.neg_beta = -kl_coef; a.exp.gamma = gamma;
-    a.exp.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
-    a.exp.rewards = rewards; a.exp.adv = adv_raw; a.exp.ret = ret; a.exp.ret_dtype = ret_dtype;
-    a.exp.stats = stats;
-    return launch_rows<kFwd>(a, dtype, 2, (hipStream_t)stream);
+    Workspace ws;
+    carve_workspace(workspace, B, T, &ws);
+    rc = launch_rows<kFwd>(a, dtype, 2, (hipStream_t)stream);
+    if (rc) return rc;
+    GaeRolloutArgs e = {};
+    e.B = int(B); e.T = int(T); e.lp = lp; e.ref_lp = ref_lp; e.values = values; e.v_dtype = v_dtype;
+    e.scores = scores; e.lengths = lengths; e.mask = mask; e.neg_beta = -kl_coef; e.gamma = gamma;
+    e.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
+    e.rewards = rewards; e.adv = adv_raw; e.ret = ret; e.ret_dtype = ret_dtype; e.stats = stats; e.ws = ws;
+    const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
+    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
+    return check_launch("k_rollout_gae");
 }
 
 extern "C" int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
@@ -625,12 +589,20 @@ extern "C" int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int
     TRLX_REQUIRE(old_lp && adv_raw && stats && values && old_values && returns && lp_out && dx && dvalues && loss &&
                      loss_stats && workspace,
                  TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_fused");
-    a.tail = 1;
-    carve_workspace(workspace, B, T, &a.ws);
-    a.lt_.values = values; a.lt_.v_dtype = v_dtype; a.lt_.old_values = old_values; a.lt_.ov_dtype = ov_dtype;
-    a.lt_.returns = returns; a.lt_.r_dtype = r_dtype; a.lt_.cv = cliprange_value; a.lt_.vf_coef = vf_coef;
-    a.lt_.dv = dvalues; a.lt_.loss = loss; a.lt_.stats = loss_stats;
-    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
+    Workspace ws;
+    carve_workspace(workspace, B, T, &ws);
+    a.tokrec = ws.tokrec;
+    a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
+    a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
+    a.ltok.dv = dvalues;
+    rc = launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
+    if (rc) return rc;
+    LossRolloutArgs L = {};
+    L.B = int(B); L.T = int(T); L.msum = stats + 3; L.vf_coef = vf_coef; L.loss = loss; L.stats = loss_stats;
+    L.ws = ws;
+    const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
+    hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, L);
+    return check_launch("k_rollout_loss");
 }
 
 extern "C" int trlx_set_tuning(const char* key, int64_t value) {
