@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "PPO experience+loss tokens/sec and % HBM roofline, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level table)
+TIMER_EVERY = 5        # instrument one step in five with per-kernel events
 
 CONFIGS = {
     # name: (rows per GPU, response tokens, vocab, description)      BASELINE.json configs[]
@@ -49,11 +50,11 @@ def algorithmic_bytes(V, s, masked):
     """Minimum HBM bytes per response token, per launch.  Each [B,T] fp32
     vector read or written once counts 4 B; int64 labels / mask 8 B."""
     mask_b = 8 if masked else 0
-    # K1: policy + ref rows, label; out lp, ref_lp; tail: values in, rewards/adv/returns out
-    exp = 2 * V * s + 8 + 2 * 4 + 4 + 3 * 4 + mask_b
-    # K2: row read + dlogits write, label, old_lp, adv, values, old_values, returns in; lp, dv out
-    loss = 2 * V * s + 8 + 4 * 6 + 2 * 4 + mask_b
-    return {"experience": exp, "loss": loss, "step": exp + loss}
+    exp = 2 * V * s + 8 + 2 * 4                     # K1 rows: policy + ref row, label -> lp, ref_lp
+    gae = 2 * 4 + 4 + 3 * 4 + mask_b               # lp, ref_lp, values -> rewards, adv, returns
+    loss = 2 * V * s + 8 + 4 * 6 + 2 * 4 + mask_b  # K2 rows: row + dlogits, label, 6 vectors -> lp, dv
+    lred = 11 * 4                                  # per-token loss record read back
+    return {"experience": exp, "loss": loss, "step": exp + gae + loss + lred}
 
 
 def make_inputs(torch, B, T, V, dev, seed, masked):
@@ -140,11 +141,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if not args.no_timers:
-        hp.timers = {}
+    # Per-kernel HIP events on every TIMER_EVERY-th step of the timed region only: an
+    # event record between two kernels costs ~10 us of queue idle on this stack (measured),
+    # so instrumenting every step would tax the number it reports.
+    timers = {}
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        hp.timers = timers if (not args.no_timers and i % TIMER_EVERY == TIMER_EVERY - 1) else None
         step()
+    hp.timers = None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -157,8 +162,8 @@ def main():
 
     # per-kernel average durations (HIP events on the launch stream, timed region only)
     kern_ms = {}
-    if hp.timers:
-        for name, evs in hp.timers.items():
+    if timers:
+        for name, evs in timers.items():
             kern_ms[name] = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     tokens = B * T
     ab = algorithmic_bytes(V, 2, masked)

@@ -156,13 +156,13 @@ int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_t T, int64_
                           float* lp_out, void* dx, int64_t dsb, int64_t dst, void* stream);
 
 /* ---------------------------------------------------------------- the fused step (2 launches)
- * Experience: policy + reference rows -> lp, ref_lp (fp32), and in the launch's tail (the
- * workgroup completing each rollout's 2T rows) the KL-penalised rewards, GAE advantages
- * (unwhitened, fp32) and returns of that rollout, plus — in the last rollout — the
- * whitening moments stats[4] = {Σ A, Σ A², n, Σ mask}.  Replaces ppo_orchestrator.py:
+ * Experience: policy + reference rows -> lp, ref_lp (fp32); then one wavefront per rollout
+ * computes its KL-penalised rewards, GAE advantages (unwhitened, fp32) and returns, and the
+ * last block the whitening moments stats[4] = {Σ A, Σ A², n, Σ mask}.  Replaces ppo_orchestrator.py:
  * 154-167 followed by ppo_models.py:121-136 (+ the moments of modeling.py:24-29).
- * Loss: new-policy rows -> lp_out, dlogits (one read + one write), and in the tail the
- * value-loss gradient dvalues and loss[1] + loss_stats[13] (order of trlx_ppo_loss_finalize),
+ * Loss: new-policy rows -> lp_out, dlogits (one read + one write), the value-loss gradient
+ * dvalues and per-token loss terms; then one wavefront per rollout sums them and the last
+ * block writes loss[1] + loss_stats[13] (order of trlx_ppo_loss_finalize),
  * i.e. ppo_models.py:141-199 with its autograd into the logits.  `stats` (possibly
  * all-reduced across ranks in between) whitens the advantages on the fly; unbiased as in
  * trlx_whiten_apply.  workspace: trlx_ppo_workspace_bytes(B, T) bytes, zero-filled once
@@ -175,6 +175,22 @@ int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dt
                               const int64_t* lengths, const int64_t* mask, float kl_coef, float gamma,
                               float lam, float* lp, float* ref_lp, float* rewards, float* adv_raw,
                               void* ret, int ret_dtype, double* stats, void* workspace, void* stream);
+/* The two launches of each fused entry point, separately (same arguments):
+ *   experience = trlx_lsm_gather_fwd(policy, ref -> fp32 lp, ref_lp) + trlx_ppo_rollout_gae
+ *   loss       = trlx_ppo_loss_rows + trlx_ppo_rollout_loss  */
+int trlx_ppo_rollout_gae(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                         int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                         float kl_coef, float gamma, float lam, float* rewards, float* adv_raw, void* ret,
+                         int ret_dtype, double* stats, void* workspace, void* stream);
+int trlx_ppo_loss_rows(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb, int64_t st,
+                       const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp, int old_dtype,
+                       const float* adv_raw, const double* stats, int unbiased, const int64_t* mask,
+                       const void* values, int v_dtype, const void* old_values, int ov_dtype,
+                       const void* returns, int r_dtype, float cliprange, float cliprange_value, float vf_coef,
+                       float* lp_out, void* dx, int64_t dsb, int64_t dst, float* dvalues, void* workspace,
+                       void* stream);
+int trlx_ppo_rollout_loss(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                          float* loss_stats, void* workspace, void* stream);
 int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
                         int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
                         int old_dtype, const float* adv_raw, const double* stats, int unbiased,

@@ -28,6 +28,9 @@ for step in "$@"; do
         bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;
         bench_c3) run bench_c3 300 python bench.py --steps 20 --warmup 5 --config c3 --cpu-seconds 0 ;;
         bench_c4) run bench_c4 300 python bench.py --steps 20 --warmup 5 --config c4 --cpu-seconds 0 ;;
+        profile_nt) run profile_nt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_nt \
+                     -o run -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-timers ;;
+        bench_nt) run bench_nt 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-timers ;;
         profile) run profile 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
                      -o run -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
         pmc_fetch) run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch \

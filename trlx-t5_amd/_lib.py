@@ -52,6 +52,13 @@ SIGNATURES = {
     "trlx_ppo_loss_finalize": (_c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_d, _c_f, _c_vp, _c_vp, _c_vp]),
     "trlx_scale_by": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
     "trlx_ppo_workspace_bytes": (_c_i64, [_c_i64, _c_i64]),
+    "trlx_ppo_rollout_gae": (_c_int, [_c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_f, _c_f,
+                                      _c_f, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
+    "trlx_ppo_loss_rows": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_i64,
+                                    _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_int,
+                                    _c_vp, _c_int, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp,
+                                    _c_vp]),
+    "trlx_ppo_rollout_loss": (_c_int, [_c_i64, _c_i64, _c_vp, _c_f, _c_vp, _c_vp, _c_vp, _c_vp]),
     "trlx_ppo_experience_fused": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                            _c_vp, _c_i64, _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_f,
                                            _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,

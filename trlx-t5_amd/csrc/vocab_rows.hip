@@ -138,10 +138,14 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
     constexpr int EPV = DT::kEPV;
     const int tid = threadIdx.x, nthr = blockDim.x;
     const Row<DT> r(a);
-    // Row-independent scalars first: their arithmetic then runs before the row occupies
-    // its VGPRs.
-    PpoScalars ps = {0.f, 1.f, 1.f, 0.f};
-    if (MODE == kPpo) ps = ppo_scalars(a, r.row);
+    // Row-independent scalars first, computed by thread 0 while the row loads are in
+    // flight and parked in LDS (read back after the reductions' barriers): they then
+    // occupy no VGPRs beside the row.
+    __shared__ float s_ps[4];
+    if (MODE == kPpo && tid == 0) {
+        const PpoScalars p0 = ppo_scalars(a, r.row);
+        s_ps[0] = p0.A; s_ps[1] = p0.m; s_ps[2] = p0.inv_msum; s_ps[3] = p0.olp;
+    }
 
     const int nvec = int(r.s.nvec);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(r.x + r.s.head, uint32_t(nvec) * 16u);
@@ -153,6 +157,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
 #pragma unroll
     for (int k = 0; k < NV; ++k)
         v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, launder_int(voff) + k * nthr * 16, 0, kAuxNT);
+    const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
     const int64_t je = r.edge_index();
     const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
 
@@ -193,7 +198,9 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
         fwd_epilogue(a, r, lse);
         return;
     }
-    const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
+
+    // (both reductions' barriers separate thread 0's s_ps writes from these reads)
+    const PpoScalars ps = {s_ps[0], s_ps[1], s_ps[2], s_ps[3]};
     PolicyTerms pt = {1.f, 0.f, 0.f, false};
     const float g = row_grad<MODE>(a, r.row, xy - lse, ps, pt);
 
@@ -201,6 +208,14 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
     const float lse_l2e = -lse * kLog2e;
     E* drow = reinterpret_cast<E*>(a.dx) + r.b * a.dsb + r.t * a.dst;
     const float gy = g * (1.0f - exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
+    // edge elements first, and the token record's inputs parked in LDS (thread 0 reads them
+    // back after the loop): fewer values live beside the row during the store loop
+    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+    __shared__ float s_tok[6];
+    if (MODE == kPpo && tid == 0) {
+        s_tok[0] = pt.ratio; s_tok[1] = pt.lr; s_tok[2] = pt.pgmax; s_tok[3] = pt.pgclip ? 1.f : 0.f;
+        s_tok[4] = ps.m; s_tok[5] = ps.inv_msum;
+    }
     if (SAME_PHASE) {
         const __amdgpu_buffer_rsrc_t rout = make_rsrc(drow + r.s.head, uint32_t(nvec) * 16u);
         const int iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? int((r.y - r.s.head) / EPV) : -1;
@@ -234,8 +249,11 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
             }
         }
     }
-    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
-    if (MODE == kPpo) token_record(a, r.row, pt, ps);
+    if (MODE == kPpo && tid == 0) {
+        const PolicyTerms t2 = {s_tok[0], s_tok[1], s_tok[2], s_tok[3] != 0.f};
+        const PpoScalars p2 = {0.f, s_tok[4], s_tok[5], 0.f};
+        token_record(a, r.row, t2, p2);
+    }
 }
 
 // ------------------------------------------------------------------ streaming rows
@@ -541,6 +559,25 @@ extern "C" int64_t trlx_ppo_workspace_bytes(int64_t B, int64_t T) {
     return int64_t(carve_workspace(nullptr, B, T, nullptr));
 }
 
+extern "C" int trlx_ppo_rollout_gae(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                                    int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                                    float kl_coef, float gamma, float lam, float* rewards, float* adv_raw, void* ret,
+                                    int ret_dtype, double* stats, void* workspace, void* stream) {
+    TRLX_REQUIRE(B > 0 && T > 0 && B * T < (1LL << 31), TRLX_ERR_SHAPE, "bad rollout batch %lld x %lld",
+                 (long long)B, (long long)T);
+    TRLX_REQUIRE(lp && ref_lp && values && rewards && adv_raw && ret && stats && workspace, TRLX_ERR_ARG,
+                 "NULL argument to trlx_ppo_rollout_gae");
+    GaeRolloutArgs e = {};
+    carve_workspace(workspace, B, T, &e.ws);
+    e.B = int(B); e.T = int(T); e.lp = lp; e.ref_lp = ref_lp; e.values = values; e.v_dtype = v_dtype;
+    e.scores = scores; e.lengths = lengths; e.mask = mask; e.neg_beta = -kl_coef; e.gamma = gamma;
+    e.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
+    e.rewards = rewards; e.adv = adv_raw; e.ret = ret; e.ret_dtype = ret_dtype; e.stats = stats;
+    const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
+    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
+    return check_launch("k_rollout_gae");
+}
+
 extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dtype, int64_t B,
                                          int64_t T, int64_t V, int64_t sb, int64_t st, const int64_t* labels,
                                          int64_t lb, int64_t lt, const void* values, int v_dtype,
@@ -548,26 +585,51 @@ extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_log
                                          float kl_coef, float gamma, float lam, float* lp, float* ref_lp,
                                          float* rewards, float* adv_raw, void* ret, int ret_dtype,
                                          double* stats, void* workspace, void* stream) {
+    TRLX_REQUIRE(ref_logits, TRLX_ERR_ARG, "NULL reference logits");
+    int rc = trlx_lsm_gather_fwd(logits, ref_logits, dtype, B, T, V, sb, st, labels, lb, lt, lp, ref_lp, TRLX_F32,
+                                 nullptr, nullptr, stream);
+    if (rc) return rc;
+    return trlx_ppo_rollout_gae(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, gamma, lam,
+                                rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
+}
+
+extern "C" int trlx_ppo_loss_rows(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
+                                  int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
+                                  int old_dtype, const float* adv_raw, const double* stats, int unbiased,
+                                  const int64_t* mask, const void* values, int v_dtype, const void* old_values,
+                                  int ov_dtype, const void* returns, int r_dtype, float cliprange,
+                                  float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb,
+                                  int64_t dst, float* dvalues, void* workspace, void* stream) {
     RowArgs a = {};
-    a.x0 = logits; a.x1 = ref_logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
-    a.labels = labels; a.lb = lb; a.lt = lt; a.lp0 = lp; a.lp1 = ref_lp; a.out_dtype = TRLX_F32;
+    a.x0 = logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
+    a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv_raw; a.stats = stats; a.unbiased = unbiased;
+    a.mask = mask; a.msum = stats ? stats + 3 : nullptr; a.msum_host = double(B * T); a.cliprange = cliprange;
+    a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
     int rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
-    TRLX_REQUIRE(ref_logits && values && lp && ref_lp && rewards && adv_raw && ret && stats && workspace,
-                 TRLX_ERR_ARG, "NULL argument to trlx_ppo_experience_fused");
+    TRLX_REQUIRE(old_lp && adv_raw && stats && values && old_values && returns && lp_out && dx && dvalues && workspace,
+                 TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_rows");
     Workspace ws;
     carve_workspace(workspace, B, T, &ws);
-    rc = launch_rows<kFwd>(a, dtype, 2, (hipStream_t)stream);
-    if (rc) return rc;
-    GaeRolloutArgs e = {};
-    e.B = int(B); e.T = int(T); e.lp = lp; e.ref_lp = ref_lp; e.values = values; e.v_dtype = v_dtype;
-    e.scores = scores; e.lengths = lengths; e.mask = mask; e.neg_beta = -kl_coef; e.gamma = gamma;
-    e.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
-    e.rewards = rewards; e.adv = adv_raw; e.ret = ret; e.ret_dtype = ret_dtype; e.stats = stats; e.ws = ws;
+    a.tokrec = ws.tokrec;
+    a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
+    a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
+    a.ltok.dv = dvalues;
+    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
+}
+
+extern "C" int trlx_ppo_rollout_loss(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                                     float* loss_stats, void* workspace, void* stream) {
+    TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
+    TRLX_REQUIRE(loss && loss_stats && workspace, TRLX_ERR_ARG, "NULL argument to trlx_ppo_rollout_loss");
+    LossRolloutArgs L = {};
+    carve_workspace(workspace, B, T, &L.ws);
+    L.B = int(B); L.T = int(T); L.msum = stats ? stats + 3 : nullptr; L.vf_coef = vf_coef; L.loss = loss;
+    L.stats = loss_stats;
     const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
-    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
-    return check_launch("k_rollout_gae");
+    hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, L);
+    return check_launch("k_rollout_loss");
 }
 
 extern "C" int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
@@ -578,31 +640,11 @@ extern "C" int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int
                                    float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb,
                                    int64_t dst, float* dvalues, float* loss, float* loss_stats, void* workspace,
                                    void* stream) {
-    RowArgs a = {};
-    a.x0 = logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
-    a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv_raw; a.stats = stats; a.unbiased = unbiased;
-    a.mask = mask; a.msum = stats ? stats + 3 : nullptr; a.msum_host = double(B * T); a.cliprange = cliprange;
-    a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
-    int rc = check_rows(a, dtype);
+    int rc = trlx_ppo_loss_rows(logits, dtype, B, T, V, sb, st, labels, lb, lt, old_lp, old_dtype, adv_raw, stats,
+                                unbiased, mask, values, v_dtype, old_values, ov_dtype, returns, r_dtype, cliprange,
+                                cliprange_value, vf_coef, lp_out, dx, dsb, dst, dvalues, workspace, stream);
     if (rc) return rc;
-    TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
-    TRLX_REQUIRE(old_lp && adv_raw && stats && values && old_values && returns && lp_out && dx && dvalues && loss &&
-                     loss_stats && workspace,
-                 TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_fused");
-    Workspace ws;
-    carve_workspace(workspace, B, T, &ws);
-    a.tokrec = ws.tokrec;
-    a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
-    a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
-    a.ltok.dv = dvalues;
-    rc = launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
-    if (rc) return rc;
-    LossRolloutArgs L = {};
-    L.B = int(B); L.T = int(T); L.msum = stats + 3; L.vf_coef = vf_coef; L.loss = loss; L.stats = loss_stats;
-    L.ws = ws;
-    const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
-    hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, L);
-    return check_launch("k_rollout_loss");
+    return trlx_ppo_rollout_loss(B, T, stats, vf_coef, loss, loss_stats, workspace, stream);
 }
 
 extern "C" int trlx_set_tuning(const char* key, int64_t value) {

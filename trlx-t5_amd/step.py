@@ -53,7 +53,7 @@ class PPOHotPath:
         nbytes = _lib.query("trlx_ppo_workspace_bytes", B, T)
         self.workspace = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)  # tickets re-armed in-kernel
         self.dlogits = None
-        self.timers = None  # optional {name: [(start_event, end_event), ...]}
+        self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
 
     # -------------------------------------------------------------- helpers
     def _ev(self, name, s):
@@ -86,14 +86,17 @@ class PPOHotPath:
         s = torch.cuda.current_stream(self.device)
         B, T, V = self.B, self.T, self.V
         self._ev("experience", s)
-        _lib.call("trlx_ppo_experience_fused", logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits),
-                  B, T, V, logits.stride(0), logits.stride(1), labels.data_ptr(), labels.stride(0),
-                  labels.stride(1), old_values.data_ptr(), _lib.dtype_code(old_values), _lib.ptr(scores),
-                  _lib.ptr(lengths), _lib.ptr(mask), self.kl_coef, float(self.cfg.gamma), float(self.cfg.lam),
-                  self.lp_old.data_ptr(), self.ref_lp.data_ptr(), self.rewards.data_ptr(), self.adv_raw.data_ptr(),
+        _lib.call("trlx_lsm_gather_fwd", logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V,
+                  logits.stride(0), logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1),
+                  self.lp_old.data_ptr(), self.ref_lp.data_ptr(), _lib.F32, None, None, s.cuda_stream)
+        self._ev_end("experience", s)
+        self._ev("rollout_gae", s)
+        _lib.call("trlx_ppo_rollout_gae", B, T, self.lp_old.data_ptr(), self.ref_lp.data_ptr(), old_values.data_ptr(),
+                  _lib.dtype_code(old_values), _lib.ptr(scores), _lib.ptr(lengths), _lib.ptr(mask), self.kl_coef,
+                  float(self.cfg.gamma), float(self.cfg.lam), self.rewards.data_ptr(), self.adv_raw.data_ptr(),
                   self.returns.data_ptr(), _lib.dtype_code(self.returns), self.adv_stats.data_ptr(),
                   self.workspace.data_ptr(), s.cuda_stream)
-        self._ev_end("experience", s)
+        self._ev_end("rollout_gae", s)
         self.distributed = dist.is_available() and dist.is_initialized()
         if self.distributed:
             dist.all_reduce(self.adv_stats[:3], dist.ReduceOp.SUM, group=group)
@@ -109,16 +112,19 @@ class PPOHotPath:
         B, T, V = self.B, self.T, self.V
         dx = self.dlogits
         self._ev("loss", s)
-        _lib.call("trlx_ppo_loss_fused", new_logits.data_ptr(), _lib.dtype_code(new_logits), B, T, V,
+        _lib.call("trlx_ppo_loss_rows", new_logits.data_ptr(), _lib.dtype_code(new_logits), B, T, V,
                   new_logits.stride(0), new_logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1),
                   self.lp_old.data_ptr(), _lib.F32, self.adv_raw.data_ptr(), self.adv_stats.data_ptr(),
                   0 if self.distributed else 1, _lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values),
                   old_values.data_ptr(), _lib.dtype_code(old_values), self.returns.data_ptr(),
                   _lib.dtype_code(self.returns), float(self.cfg.cliprange), float(self.cfg.cliprange_value),
                   float(self.cfg.vf_coef), self.lp_new.data_ptr(), dx.data_ptr(), dx.stride(0), dx.stride(1),
-                  self.dvalues.data_ptr(), self.loss.data_ptr(), self.stats.data_ptr(), self.workspace.data_ptr(),
-                  s.cuda_stream)
+                  self.dvalues.data_ptr(), self.workspace.data_ptr(), s.cuda_stream)
         self._ev_end("loss", s)
+        self._ev("rollout_loss", s)
+        _lib.call("trlx_ppo_rollout_loss", B, T, self.adv_stats.data_ptr(), float(self.cfg.vf_coef),
+                  self.loss.data_ptr(), self.stats.data_ptr(), self.workspace.data_ptr(), s.cuda_stream)
+        self._ev_end("rollout_loss", s)
         return self.loss, self.stats, self.dlogits, self.dvalues
 
     def step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
