@@ -225,6 +225,56 @@ int trlx_ppo_loss_finalize(const double* partials, int64_t nblk, int64_t n,
                            const double* msum, double msum_host, float vf_coef,
                            float* loss, float* stats, void* stream);
 
+/* ---------------------------------------------------------------- A10 (ILQL loss)
+ * ILQLConfig.loss — replaces trlx/model/nn/ilql_models.py:52-116 with its autograd
+ * (config 5).  Every vocab row (logits [B,L,V] and the nq Q-head rows [B,A,V]) is read
+ * once into registers and its gradient row written once:
+ *   logits row (b,t<L-1): CE against input_ids[b,t+1], weight attention_mask[b,t+1]
+ *                         (AWAC, :98-105); row t = L-1 gets a zero gradient
+ *   q_i row (b,a)       : CE against the action a* = input_ids[b, 1+actions_ixs[b,a]]
+ *                         weighted by dones[b,a] (CQL, :87-96) + the TD term
+ *                         ((Q_i[a*] - (r + gamma*vs[b,a+1]*dones[b,a+1]))*dones[b,a])^2 (:63-74)
+ *   target-Q rows are only gathered at a* (min over heads) for the expectile V loss (:76-83).
+ * Three launches: prep (n_nonterminal = max(1, sum dones[:, :-1]) and sum attention[:, 1:]),
+ * rows (one workgroup per vocab row), finalize (fixed-order fp64 sums -> losses[5] =
+ * {loss, loss_q, loss_v, loss_cql, loss_awac}).  dvs = d loss / d vs (fp32 [B, A+1], last
+ * column 0).  Gradient rows have the same strides and 16-B phase as their inputs.  The
+ * small [B, .] tensors are contiguous.  No collective: the reference's ILQL loss is
+ * rank-local (DDP averages the gradients). */
+typedef struct {
+    int dtype;                        /* TRLX_F32 / TRLX_BF16: logits, q, tq rows */
+    int nq;                           /* 1 or 2 Q heads (ILQLConfig.two_qs) */
+    int64_t B, L, A, V;               /* rows, tokens, actions (states = A + 1), vocab */
+    const void* logits;               /* [B,L,V], row (b,t) at logits + b*logits_sb + t*logits_st */
+    int64_t logits_sb, logits_st;
+    const void* q[2];                 /* [B,A,V] Q heads (q[1] unused when nq == 1) */
+    int64_t q_sb[2], q_st[2];
+    const void* tq[2];                /* [B,A,V] target Q heads (gathered only) */
+    int64_t tq_sb[2], tq_st[2];
+    const int64_t* input_ids;         /* [B,L] */
+    const int64_t* attention_mask;    /* [B,L] */
+    const int64_t* actions_ixs;       /* [B,A] */
+    const int64_t* dones;             /* [B,A+1] */
+    const void* rewards;              /* [B,A] */
+    int rewards_dtype;
+    const void* vs;                   /* [B,A+1] (the reference's [B,S,1]) */
+    int vs_dtype;
+    float tau, gamma, cql_scale, awac_scale;
+    void* dlogits;                    /* gradient rows, dtype of the inputs */
+    int64_t dlogits_sb, dlogits_st;
+    void* dq[2];
+    int64_t dq_sb[2], dq_st[2];
+    float* dvs;                       /* [B,A+1] fp32 */
+    float* losses;                    /* [5] fp32 */
+    void* workspace;                  /* trlx_ilql_workspace_bytes(B, L, A, nq) bytes */
+} trlx_ilql_args;
+
+int64_t trlx_ilql_workspace_bytes(int64_t B, int64_t L, int64_t A, int nq);
+int trlx_ilql_prep(const trlx_ilql_args* args, void* stream);
+int trlx_ilql_rows(const trlx_ilql_args* args, void* stream);
+int trlx_ilql_finalize(const trlx_ilql_args* args, void* stream);
+int trlx_ilql_loss_fused(const trlx_ilql_args* args, void* stream);   /* the three in order */
+
 /* ---------------------------------------------------------------- autograd plumbing
  * out[i] = x[i] * (*scale) for i < n (scale: device fp32 scalar, e.g. a backward's
  * grad_output).  In place (out == x) it is skipped entirely when *scale == 1. */

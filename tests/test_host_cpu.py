@@ -131,3 +131,28 @@ def test_dp_whitening_statistics_gloo(golden, world):
         assert cnt == float(z[f"f32_big/dist{world}/count"])
         w = (xs - mean) * torch.rsqrt(torch.tensor(var, dtype=torch.float32) + 1e-8)
         torch.testing.assert_close(w, T(z[f"f32_big/dist{world}/whiten"]), rtol=1e-5, atol=1e-5)
+
+
+def test_ilql_args_layout_matches_header(tmp_path):
+    """The ctypes mirror of trlx_ilql_args has the C compiler's field offsets."""
+    fields = [f[0] for f in _lib.IlqlArgs._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "trlx_t5_amd.h"\nint main(void){\n'
+                   + "".join(f'printf("%zu\\n", offsetof(trlx_ilql_args, {f}));\n' for f in fields)
+                   + 'printf("%zu\\n", sizeof(trlx_ilql_args));\nreturn 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).decode().split()]
+    want = [getattr(_lib.IlqlArgs, f).offset for f in fields] + [__import__("ctypes").sizeof(_lib.IlqlArgs)]
+    assert got == want
+
+
+def test_ilql_refuses_cpu_tensors():
+    cfg = P.ILQLConfig()
+    B, L, V = 2, 4, 7
+    A = L - 1
+    b = P.ILQLBatch(torch.zeros(B, L, dtype=torch.long), torch.ones(B, L, dtype=torch.long), torch.zeros(B, A),
+                    torch.arange(L).repeat(B, 1), torch.arange(A).repeat(B, 1), torch.ones(B, L, dtype=torch.long))
+    qs = [torch.randn(B, A, V) for _ in range(2)]
+    with pytest.raises(ValueError, match="ROCm"):
+        cfg.loss((torch.randn(B, L, V), (qs, qs, torch.randn(B, L, 1))), b)

@@ -22,6 +22,27 @@ PPO_PARTIAL_SLOTS = 16
 
 _c_vp, _c_i64, _c_int, _c_f, _c_d = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double
 
+
+class IlqlArgs(ctypes.Structure):
+    """Mirror of trlx_ilql_args (include/trlx_t5_amd.h)."""
+    _fields_ = [
+        ("dtype", _c_int), ("nq", _c_int),
+        ("B", _c_i64), ("L", _c_i64), ("A", _c_i64), ("V", _c_i64),
+        ("logits", _c_vp), ("logits_sb", _c_i64), ("logits_st", _c_i64),
+        ("q", _c_vp * 2), ("q_sb", _c_i64 * 2), ("q_st", _c_i64 * 2),
+        ("tq", _c_vp * 2), ("tq_sb", _c_i64 * 2), ("tq_st", _c_i64 * 2),
+        ("input_ids", _c_vp), ("attention_mask", _c_vp), ("actions_ixs", _c_vp), ("dones", _c_vp),
+        ("rewards", _c_vp), ("rewards_dtype", _c_int),
+        ("vs", _c_vp), ("vs_dtype", _c_int),
+        ("tau", _c_f), ("gamma", _c_f), ("cql_scale", _c_f), ("awac_scale", _c_f),
+        ("dlogits", _c_vp), ("dlogits_sb", _c_i64), ("dlogits_st", _c_i64),
+        ("dq", _c_vp * 2), ("dq_sb", _c_i64 * 2), ("dq_st", _c_i64 * 2),
+        ("dvs", _c_vp), ("losses", _c_vp), ("workspace", _c_vp),
+    ]
+
+
+_ilql_p = ctypes.POINTER(IlqlArgs)
+
 # name -> (restype, argtypes)   (must match include/trlx_t5_amd.h exactly)
 SIGNATURES = {
     "trlx_abi_version": (_c_int, []),
@@ -67,6 +88,11 @@ SIGNATURES = {
                                      _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                                      _c_vp, _c_int, _c_vp, _c_int, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_i64,
                                      _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "trlx_ilql_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_int]),
+    "trlx_ilql_prep": (_c_int, [_ilql_p, _c_vp]),
+    "trlx_ilql_rows": (_c_int, [_ilql_p, _c_vp]),
+    "trlx_ilql_finalize": (_c_int, [_ilql_p, _c_vp]),
+    "trlx_ilql_loss_fused": (_c_int, [_ilql_p, _c_vp]),
 }
 
 _lib = None

@@ -1,0 +1,178 @@
+"""Drop-in for the ILQL loss of trlx/model/nn/ilql_models.py (config 5) on MI355X.
+
+  ILQLConfig        ilql_models.py:37-58  (method config; .loss on HIP kernels)
+  ILQLConfig.loss   ilql_models.py:52-116 (CQL / AWAC cross-entropies over V, TD and
+                                           expectile V losses, with autograd)
+  ILQLBatch         trlx/data/ilql_types.py:30-49
+
+The loss runs as three launches (include/trlx_t5_amd.h, trlx_ilql_*): every logits row and
+every Q-head row is read once and its gradient row written once in the forward; the
+autograd backward only scales the stored gradients by grad_output (a no-op for 1).
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import Any, Sequence
+
+import torch
+
+from . import _lib
+from .modeling import grad_buffer_like
+
+__all__ = ["ILQLConfig", "ILQLBatch", "ILQL_LOSS_KEYS"]
+
+# stats keys in the reference's order (its dict comprehension walks locals(): loss_q,
+# loss_v, loss_cql, loss_awac, loss — ilql_models.py:109-113)
+ILQL_LOSS_KEYS = ("losses/loss_q", "losses/loss_v", "losses/loss_cql", "losses/loss_awac", "losses/loss")
+_SLOT = {"losses/loss": 0, "losses/loss_q": 1, "losses/loss_v": 2, "losses/loss_cql": 3, "losses/loss_awac": 4}
+
+
+@dataclass
+class ILQLBatch:
+    """Batched ILQL elements (trlx/data/ilql_types.py:30-49)."""
+    input_ids: torch.Tensor       # [B, L] int64
+    attention_mask: torch.Tensor  # [B, L]
+    rewards: torch.Tensor         # [B, A]
+    states_ixs: torch.Tensor      # [B, S]
+    actions_ixs: torch.Tensor     # [B, A]
+    dones: torch.Tensor           # [B, S]
+
+
+def _row_view(x, name, shape3):
+    if x.dim() != 3 or tuple(x.shape) != tuple(shape3):
+        raise ValueError(f"{name} must have shape {tuple(shape3)}, got {tuple(x.shape)}")
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    return x
+
+
+def _strides(x):
+    return x.stride(0), x.stride(1)
+
+
+class _ILQLLoss(torch.autograd.Function):
+    """Forward = trlx_ilql_loss_fused (gradients computed eagerly, closed form); backward
+    scales the stored gradients in place by grad_output."""
+
+    @staticmethod
+    def forward(ctx, cfg, logits, vs, q0, q1, tq0, tq1, batch):
+        dev = logits.device
+        B, L, V = logits.shape
+        nq = 1 if q1 is None else 2
+        A = q0.shape[1]
+        S = A + 1
+        lg = _row_view(logits, "logits", (B, L, V))
+        qs = [_row_view(q, f"qs[{i}]", (B, A, V)) for i, q in enumerate((q0, q1)[:nq])]
+        tqs = [_row_view(q, f"target_qs[{i}]", (B, A, V)) for i, q in enumerate((tq0, tq1)[:nq])]
+        for t in qs + tqs:
+            if t.dtype != lg.dtype:
+                raise TypeError("logits, qs and target_qs must share one dtype")
+        vflat = vs.reshape(B, S) if vs.numel() == B * S else None
+        if vflat is None:
+            raise ValueError(f"vs must hold [B, A+1] = [{B}, {S}] values, got {tuple(vs.shape)}")
+        vflat = vflat.contiguous()
+        if vflat.dtype not in (torch.float32, torch.bfloat16):
+            vflat = vflat.float()
+        ids = batch.input_ids.to(device=dev, dtype=torch.int64).contiguous()
+        attn = batch.attention_mask.to(device=dev, dtype=torch.int64).contiguous()
+        aix = batch.actions_ixs.to(device=dev, dtype=torch.int64).contiguous()
+        dones = batch.dones.to(device=dev, dtype=torch.int64).contiguous()
+        rew = batch.rewards.to(device=dev).contiguous()
+        if rew.dtype not in (torch.float32, torch.bfloat16):
+            rew = rew.float()
+        for name, t, shp in (("input_ids", ids, (B, L)), ("attention_mask", attn, (B, L)),
+                             ("actions_ixs", aix, (B, A)), ("dones", dones, (B, S)), ("rewards", rew, (B, A))):
+            if tuple(t.shape) != shp:
+                raise ValueError(f"batch.{name} must have shape {shp}, got {tuple(t.shape)}")
+
+        dlg = grad_buffer_like(lg)
+        dqs = [grad_buffer_like(q) for q in qs]
+        dvs = torch.empty((B, S), dtype=torch.float32, device=dev)
+        losses = torch.empty(5, dtype=torch.float32, device=dev)
+        ws = torch.empty(_lib.query("trlx_ilql_workspace_bytes", B, L, A, nq), dtype=torch.uint8, device=dev)
+
+        a = _lib.IlqlArgs()
+        a.dtype, a.nq, a.B, a.L, a.A, a.V = _lib.dtype_code(lg), nq, B, L, A, V
+        a.logits = lg.data_ptr()
+        a.logits_sb, a.logits_st = _strides(lg)
+        a.dlogits = dlg.data_ptr()
+        a.dlogits_sb, a.dlogits_st = _strides(dlg)
+        for i in range(nq):
+            a.q[i], a.tq[i], a.dq[i] = qs[i].data_ptr(), tqs[i].data_ptr(), dqs[i].data_ptr()
+            a.q_sb[i], a.q_st[i] = _strides(qs[i])
+            a.tq_sb[i], a.tq_st[i] = _strides(tqs[i])
+            a.dq_sb[i], a.dq_st[i] = _strides(dqs[i])
+        a.input_ids, a.attention_mask, a.actions_ixs, a.dones = (ids.data_ptr(), attn.data_ptr(), aix.data_ptr(),
+                                                                 dones.data_ptr())
+        a.rewards, a.rewards_dtype = rew.data_ptr(), _lib.dtype_code(rew)
+        a.vs, a.vs_dtype = vflat.data_ptr(), _lib.dtype_code(vflat)
+        a.tau, a.gamma, a.cql_scale, a.awac_scale = (float(cfg.tau), float(cfg.gamma), float(cfg.cql_scale),
+                                                     float(cfg.awac_scale))
+        a.dvs, a.losses, a.workspace = dvs.data_ptr(), losses.data_ptr(), ws.data_ptr()
+        _lib.call("trlx_ilql_loss_fused", ctypes.byref(a), _lib.stream_of(lg))
+
+        ctx.grads = [dlg] + dqs
+        ctx.dvs = dvs
+        ctx.meta = (logits.shape, [q.shape for q in (q0, q1)[:nq]], vs.shape, vs.dtype, nq)
+        ctx.mark_non_differentiable(losses)
+        return losses[0].clone(), losses
+
+    @staticmethod
+    def backward(ctx, grad_loss, grad_stats):
+        if ctx.grads is None:
+            raise RuntimeError("ILQL loss backward called twice (gradients are scaled in place)")
+        grads, ctx.grads = ctx.grads, None
+        g = grad_loss.to(torch.float32).reshape(1).contiguous()
+        for t in grads:  # whole backing buffer; the kernel returns at once when grad_output == 1
+            buf = t if t._base is None else t._base
+            _lib.call("trlx_scale_by", _lib.ptr(buf), _lib.ptr(buf), _lib.dtype_code(buf), buf.numel(),
+                      _lib.ptr(g), _lib.stream_of(buf))
+        dvs = ctx.dvs
+        _lib.call("trlx_scale_by", _lib.ptr(dvs), _lib.ptr(dvs), _lib.F32, dvs.numel(), _lib.ptr(g),
+                  _lib.stream_of(dvs))
+        lshape, qshapes, vshape, vdtype, nq = ctx.meta
+        dvs = dvs.view(vshape).to(vdtype)
+        dq = grads[1:] + [None] * (2 - nq)
+        return None, grads[0], dvs, dq[0], dq[1], None, None, None
+
+
+@dataclass
+class ILQLConfig:
+    """ILQL method config (ilql_models.py:37-49) with the loss on MI355X."""
+
+    name: str = "ilqlconfig"
+    tau: float = 0.7
+    gamma: float = 0.99
+    cql_scale: float = 0.1
+    awac_scale: float = 1.0
+    alpha: float = 0.001
+    steps_for_target_q_sync: float = 5
+    betas: Sequence[float] = (4,)
+    two_qs: bool = True
+
+    @classmethod
+    def from_dict(cls, config: dict):
+        return cls(**config)
+
+    def loss(self, outputs: Any, labels: ILQLBatch):
+        """ILQLConfig.loss (ilql_models.py:52-116): outputs = (logits, (qs, target_qs, vs)).
+
+        Returns (loss, stats) with the reference's stats keys; stats values are 0-d device
+        tensors ("losses/loss" is the loss itself).  Gradients reach logits, qs and vs.
+        Deviation: with one action per row (A == 1) and B > 1 the reference's
+        `vs[:, :-1].squeeze()` drops the action axis and broadcasts [B,1] against [B]
+        into a [B,B] loss; that degenerate shape raises ValueError here."""
+        logits, (qs, target_qs, vs) = outputs
+        qs, target_qs = list(qs), list(target_qs)
+        if len(qs) not in (1, 2) or len(target_qs) != len(qs):
+            raise ValueError("ILQL needs 1 or 2 Q heads and as many target heads")
+        _lib.require_cuda(logits, vs, *qs, *target_qs)
+        B, A = qs[0].shape[0], qs[0].shape[1]
+        if A == 1 and B > 1:
+            raise ValueError("A == 1 with B > 1: the reference's squeeze() broadcasts [B,1] against [B] "
+                             "(ilql_models.py:70-72); unsupported")
+        q1 = qs[1] if len(qs) > 1 else None
+        tq1 = target_qs[1] if len(qs) > 1 else None
+        loss, losses = _ILQLLoss.apply(self, logits, vs, qs[0], q1, target_qs[0].detach(),
+                                       None if tq1 is None else tq1.detach(), labels)
+        stats = {k: (loss if k == "losses/loss" else losses[_SLOT[k]]) for k in ILQL_LOSS_KEYS}
+        return loss, stats
