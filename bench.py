@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — PPO experience+loss hot path throughput on MI355X.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4] [--cpu-seconds S]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--cpu-seconds S]
 
 One "step" = one PPOHotPath.step over one shard of synthetic rollouts (see
 trlx-t5_amd/step.py): policy+reference log-softmax-gather (experience), fused KL reward
@@ -9,6 +9,9 @@ trlx-t5_amd/step.py): policy+reference log-softmax-gather (experience), fused KL
 gradient + dlogits write, value loss + stats.  Inputs are resident in HBM before timing.
 Weak scaling: every rank processes its own shard of the configuration's per-GPU batch;
 `value` = all ranks' tokens / max-over-ranks wall time.
+
+--config c5 times the ILQL loss instead (ILQLHotPath.step: prep, rows, finalize launches;
+tokens = action tokens; no collective — the reference's ILQL loss is rank-local).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
   roofline      dominant kernel's algorithmic bytes / its average HIP-event time vs 8 TB/s
@@ -24,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "PPO experience+loss tokens/sec and % HBM roofline, 1/2/4/8 MI355X"
+METRIC_ILQL = "ILQL loss (fwd+bwd) action tokens/sec and % HBM roofline, MI355X (config 5, not the headline)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level table)
 TIMER_EVERY = 5        # instrument one step in five with per-kernel events
 
@@ -32,6 +36,8 @@ CONFIGS = {
     "c2": (128, 48, 50257, "C2 GPT-2 sentiments PPO shape: 128 x 48 response tokens, vocab 50257, bf16 logits"),
     "c3": (256, 48, 32128, "C3 T5-base seq2seq PPO: 256 rows/GPU x 48 decoder tokens (decoder-length masked), vocab 32128"),
     "c4": (128, 128, 32128, "C4 UL2-20B rl_ul2 shape: 128 rows/GPU x 128 decoder tokens, vocab 32128, bf16 logits"),
+    "c5": (128, 64, 50257, "C5 ILQL sentiments loss: 128 rows/GPU x 64 tokens (63 actions), vocab 50257, fp32 "
+                           "logits + 2 Q + 2 target-Q heads"),
 }
 
 
@@ -57,6 +63,74 @@ def algorithmic_bytes(V, s, masked):
     return {"experience": exp, "loss": loss, "step": exp + gae + loss + lred}
 
 
+def ilql_algorithmic_bytes(B, L, V, s, nq=2):
+    """Minimum HBM bytes of one ILQL rows launch: every logits row but the last and every
+    Q row read once, every gradient row written once (the last logits row's gradient is
+    zeros, write-only); target-Q rows cost two 4-B gathers per action; small [B, .] tensors
+    (ids, masks, rewards, vs, dvs, records) read / written once."""
+    A = L - 1
+    rows = (B * (L - 1) + nq * B * A) * V * s + (B * L + nq * B * A) * V * s
+    small = B * A * (nq * s + 8 + 8 + 4 + 4 + 4 + 16 * (1 + nq)) + B * L * (8 + 8)
+    return rows + small
+
+
+def make_ilql_inputs(torch, P, B, L, V, dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    A = L - 1
+    f = dict(generator=g, device=dev)
+    logits = torch.randn(B, L, V, **f)
+    qs = [torch.randn(B, A, V, **f) for _ in range(2)]
+    tqs = [q + 0.1 * torch.randn(B, A, V, **f) for q in qs]
+    vs = torch.randn(B, L, **f)
+    ids = torch.randint(0, V, (B, L), **f)
+    dones = torch.ones(B, L, dtype=torch.long, device=dev)
+    dones[:, -1] = 0
+    batch = P.ILQLBatch(ids, torch.ones(B, L, dtype=torch.long, device=dev), torch.randn(B, A, **f),
+                        torch.arange(L, device=dev).repeat(B, 1), torch.arange(A, device=dev).repeat(B, 1), dones)
+    torch.cuda.synchronize()
+    return logits, qs, tqs, vs, batch
+
+
+def ilql_cpu_baseline(torch, L, V, seconds):
+    """Oracle ILQL loss (reference ops, fp32, autograd backward) on host cores."""
+    from oracle import ppo_oracle as orc
+    cores = _cores()
+    torch.set_num_threads(cores)
+    Bs, A = 2, L - 1
+    g = torch.Generator().manual_seed(123)
+    logits = torch.randn(Bs, L, V, generator=g)
+    qs = [torch.randn(Bs, A, V, generator=g) for _ in range(2)]
+    tqs = [torch.randn(Bs, A, V, generator=g) for _ in range(2)]
+    vs = torch.randn(Bs, L, 1, generator=g)
+    ids = torch.randint(0, V, (Bs, L), generator=g)
+    dones = torch.ones(Bs, L, dtype=torch.long)
+    dones[:, -1] = 0
+    rew = torch.randn(Bs, A, generator=g)
+    toks, t0 = 0, time.perf_counter()
+    while True:
+        lg = logits.clone().requires_grad_(True)
+        q = [x.clone().requires_grad_(True) for x in qs]
+        v = vs.clone().requires_grad_(True)
+        loss, _ = orc.ilql_loss(lg, q, tqs, v, ids, torch.ones(Bs, L, dtype=torch.long), rew,
+                                torch.arange(A).repeat(Bs, 1), dones)
+        loss.backward()
+        toks += Bs * A
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": toks / el, "unit": "tokens/s", "cores": cores, "kind": "port",
+            "sample": f"{toks // (Bs * A)} steps of {Bs}x{L}x{V} fp32 (oracle.ilql_loss: reference ops incl. "
+                      f"autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
+
+
+def _cores():
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    return max(1, min(cores, 16))
+
+
 def make_inputs(torch, B, T, V, dev, seed, masked):
     g = torch.Generator(device=dev).manual_seed(seed)
     bf = torch.bfloat16
@@ -80,11 +154,7 @@ def make_inputs(torch, B, T, V, dev, seed, masked):
 def cpu_baseline(torch, T, V, seconds):
     """Oracle (reference PyTorch ops, native bf16 like the T5/UL2 path) on host cores."""
     from oracle import ppo_oracle as orc
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    cores = _cores()
     torch.set_num_threads(cores)
     Bs = 8
     g = torch.Generator().manual_seed(123)
@@ -127,13 +197,21 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     B, T, V, desc = CONFIGS[args.config]
+    ilql = args.config == "c5"
     masked = args.config == "c3"
-    x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked)
-    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05)
+    if ilql:
+        lg, qs, tqs, vs, batch = make_ilql_inputs(torch, P, B, T, V, dev, seed=1000 + rank)
+        hp = P.ILQLHotPath(P.ILQLConfig(), B, T, V, torch.float32, dev)
 
-    def step():
-        return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],
-                       x["values"], x["scores"], lengths=x["lengths"], mask=x["mask"])
+        def step():
+            return hp.step(lg, qs, tqs, vs, batch)
+    else:
+        x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked)
+        hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05)
+
+        def step():
+            return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],
+                           x["values"], x["scores"], lengths=x["lengths"], mask=x["mask"])
 
     for _ in range(args.warmup):
         step()
@@ -165,11 +243,18 @@ def main():
     if timers:
         for name, evs in timers.items():
             kern_ms[name] = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-    tokens = B * T
-    ab = algorithmic_bytes(V, 2, masked)
+    if ilql:  # action tokens; per-launch bytes of the rows kernel
+        tokens = B * (T - 1)
+        ab = {"rows": ilql_algorithmic_bytes(B, T, V, 4) / tokens}
+        ab["step"] = ab["rows"]
+        doms = ("rows",)
+    else:
+        tokens = B * T
+        ab = algorithmic_bytes(V, 2, masked)
+        doms = ("experience", "loss")
     roof = None
     if kern_ms:
-        dom = max(("experience", "loss"), key=lambda k: kern_ms.get(k, 0.0))
+        dom = max(doms, key=lambda k: kern_ms.get(k, 0.0))
         ach = ab[dom] * tokens / (kern_ms[dom] * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -179,7 +264,7 @@ def main():
             traffic = rec.get(args.config, {}).get(dom)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
-                "bytes_per_launch": ab[dom] * tokens, "avg_launch_us": round(kern_ms[dom] * 1e3, 2),
+                "bytes_per_launch": int(round(ab[dom] * tokens)), "avg_launch_us": round(kern_ms[dom] * 1e3, 2),
                 "kernels_avg_us": {k: round(v * 1e3, 2) for k, v in kern_ms.items()},
                 "step_frac": round(ab["step"] * tokens / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
 
@@ -187,10 +272,10 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(torch, T, V, args.cpu_seconds)
+            cpu = (ilql_cpu_baseline if ilql else cpu_baseline)(torch, T, V, args.cpu_seconds)
         ms = elapsed / args.steps * 1e3
         out = {
-            "metric": METRIC,
+            "metric": METRIC_ILQL if ilql else METRIC,
             "value": round(world * tokens * args.steps / elapsed, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -200,10 +285,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32",  # arithmetic type; logits_dtype in config
             "data": "synthetic",
             "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world, "seq_len": T, "vocab": V,
-                       "logits_dtype": "bf16", "tokens_per_gpu_step": tokens, "parallelism": f"dp{world}"},
+                       "logits_dtype": "fp32" if ilql else "bf16", "tokens_per_gpu_step": tokens,
+                       "parallelism": f"dp{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -20,14 +20,14 @@ from .modeling import (RunningMoments, flatten_dict, get_global_statistics, grad
                        logprobs_from_logits, moments, whiten)
 from .ppo import (STATS_KEYS, AdaptiveKLController, FixedKLController, PPOConfig, kl_penalty_rewards,
                   prepare_scores, stats_dict)
-from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig
+from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig, ILQLHotPath
 from .step import PPOHotPath
 
 __all__ = [
     "logprobs_from_logits", "whiten", "get_global_statistics", "RunningMoments", "flatten_dict", "moments",
     "grad_buffer_like", "PPOConfig", "AdaptiveKLController", "FixedKLController", "kl_penalty_rewards",
     "prepare_scores", "stats_dict", "STATS_KEYS", "PPOHotPath", "load_library",
-    "ILQLConfig", "ILQLBatch", "ILQL_LOSS_KEYS",
+    "ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS",
 ]
 
 

@@ -18,7 +18,7 @@ import torch
 from . import _lib
 from .modeling import grad_buffer_like
 
-__all__ = ["ILQLConfig", "ILQLBatch", "ILQL_LOSS_KEYS"]
+__all__ = ["ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS"]
 
 # stats keys in the reference's order (its dict comprehension walks locals(): loss_q,
 # loss_v, loss_cql, loss_awac, loss — ilql_models.py:109-113)
@@ -176,3 +176,70 @@ class ILQLConfig:
                                        None if tq1 is None else tq1.detach(), labels)
         stats = {k: (loss if k == "losses/loss" else losses[_SLOT[k]]) for k in ILQL_LOSS_KEYS}
         return loss, stats
+
+
+class ILQLHotPath:
+    """Device-resident ILQL loss step for one data-parallel shard (bench / training loop):
+    gradient buffers and workspace allocated once per shape; one `step` is the three
+    trlx_ilql_* launches (prep, rows, finalize) and allocates nothing.  The reference's
+    ILQL loss has no collective (rank-local loss, DDP averages gradients), so shards are
+    independent replicas."""
+
+    def __init__(self, cfg: ILQLConfig, B: int, L: int, V: int, dtype: torch.dtype, device):
+        self.cfg = cfg
+        self.B, self.L, self.V, self.A = B, L, V, L - 1
+        self.nq = 2 if cfg.two_qs else 1
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.dvs = torch.empty((B, self.A + 1), dtype=torch.float32, device=self.device)
+        self.losses = torch.empty(5, dtype=torch.float32, device=self.device)
+        nbytes = _lib.query("trlx_ilql_workspace_bytes", B, L, self.A, self.nq)
+        self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self.dlogits = None
+        self.dq = None
+        self.timers = None  # optional {name: [[start_event, end_event], ...]}
+
+    def _timed(self, name, s, fn):
+        if self.timers is None:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        fn()
+        e1.record(s)
+        self.timers.setdefault(name, []).append([e0, e1])
+
+    def step(self, logits, qs, target_qs, vs, batch: ILQLBatch):
+        B, L, V, A, nq = self.B, self.L, self.V, self.A, self.nq
+        if tuple(logits.shape) != (B, L, V) or logits.dtype != self.dtype or logits.stride(-1) != 1:
+            raise ValueError("logits do not match the hot path shape / dtype")
+        for q in list(qs) + list(target_qs):
+            if tuple(q.shape) != (B, A, V) or q.dtype != self.dtype or q.stride(-1) != 1:
+                raise ValueError("Q heads must be [B, L-1, V] of the logits dtype")
+        if self.dlogits is None or self.dlogits.stride() != logits.stride():
+            self.dlogits = grad_buffer_like(logits)
+            self.dq = [grad_buffer_like(q) for q in qs[:nq]]
+        a = _lib.IlqlArgs()
+        a.dtype, a.nq, a.B, a.L, a.A, a.V = _lib.dtype_code(logits), nq, B, L, A, V
+        a.logits, (a.logits_sb, a.logits_st) = logits.data_ptr(), _strides(logits)
+        a.dlogits, (a.dlogits_sb, a.dlogits_st) = self.dlogits.data_ptr(), _strides(self.dlogits)
+        for i in range(nq):
+            a.q[i], a.tq[i], a.dq[i] = qs[i].data_ptr(), target_qs[i].data_ptr(), self.dq[i].data_ptr()
+            a.q_sb[i], a.q_st[i] = _strides(qs[i])
+            a.tq_sb[i], a.tq_st[i] = _strides(target_qs[i])
+            a.dq_sb[i], a.dq_st[i] = _strides(self.dq[i])
+        for name in ("input_ids", "attention_mask", "actions_ixs", "dones"):
+            t = getattr(batch, name)
+            if t.dtype != torch.int64 or not t.is_contiguous():
+                raise ValueError(f"batch.{name} must be contiguous int64")
+            setattr(a, name, t.data_ptr())
+        a.rewards, a.rewards_dtype = batch.rewards.data_ptr(), _lib.dtype_code(batch.rewards)
+        a.vs, a.vs_dtype = vs.data_ptr(), _lib.dtype_code(vs)
+        a.tau, a.gamma = float(self.cfg.tau), float(self.cfg.gamma)
+        a.cql_scale, a.awac_scale = float(self.cfg.cql_scale), float(self.cfg.awac_scale)
+        a.dvs, a.losses, a.workspace = self.dvs.data_ptr(), self.losses.data_ptr(), self.workspace.data_ptr()
+        s = torch.cuda.current_stream(self.device)
+        ref = ctypes.byref(a)
+        self._timed("prep", s, lambda: _lib.call("trlx_ilql_prep", ref, s.cuda_stream))
+        self._timed("rows", s, lambda: _lib.call("trlx_ilql_rows", ref, s.cuda_stream))
+        self._timed("finalize", s, lambda: _lib.call("trlx_ilql_finalize", ref, s.cuda_stream))
+        return self.losses, self.dlogits, self.dq, self.dvs

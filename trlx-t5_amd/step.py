@@ -1,17 +1,19 @@
 """The PPO experience + loss hot path for one data-parallel shard, device resident.
 
-One `PPOHotPath.step` is TWO kernel launches (plus, when world > 1, one 24-byte RCCL
-all-reduce between them):
+One `PPOHotPath.step` is four kernel launches (plus, when world > 1, one 24-byte RCCL
+all-reduce between the two halves):
 
-  K1  trlx_ppo_experience_fused   (ppo_orchestrator.py:154-167 + ppo_models.py:121-136)
-      policy + reference logits rows -> lp, ref_lp                     (2 x V*s read / token)
-      tail: the workgroup completing each rollout's 2T rows computes its KL-penalised
-      rewards, GAE advantages and returns; the last rollout reduces the whitening
-      moments {Σ A, Σ A², n, Σ mask}
+  experience  trlx_lsm_gather_fwd          policy + reference logits rows -> lp, ref_lp
+                                           (2 x V*s read / token; ppo_orchestrator.py:154-155)
+              trlx_ppo_rollout_gae         one wave per rollout: KL-penalised rewards, GAE
+                                           advantages + returns, whitening moments
+                                           {Σ A, Σ A², n, Σ mask} (ppo_orchestrator.py:163-167,
+                                           ppo_models.py:121-136, modeling.py:24-29)
       [RCCL all-reduce of {Σ A, Σ A², n} when world > 1 -- the only data-path exchange]
-  K2  trlx_ppo_loss_fused         (accelerate_ppo_model.py:108-126 -> ppo_models.py:141-199)
-      new-policy rows -> lp_new, PPO policy gradient, dlogits      (V*s read + V*s write / token)
-      tail: value-loss gradient, per-rollout loss sums, last rollout -> loss + 13 stats
+  loss        trlx_ppo_loss_rows           new-policy rows -> lp_new, PPO policy gradient,
+                                           dlogits (V*s read + V*s write / token), d values,
+                                           per-token loss terms (ppo_models.py:141-199)
+              trlx_ppo_rollout_loss        fixed-order loss sums -> loss + 13 stats
       [RCCL all-reduce of the stats vector for logging when world > 1]
 
 Buffers (and the zero-filled ticket workspace) are allocated once per shape; a step
@@ -137,4 +139,5 @@ class PPOHotPath:
         out = self.policy_loss(new_logits, labels, values, old_values, mask=mask)
         if reduce_stats and self.distributed:
             dist.all_reduce(self.stats, dist.ReduceOp.SUM, group=group)  # logging: mean over ranks
+            self.stats.div_(dist.get_world_size(group))
         return out
