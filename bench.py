@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 METRIC = "PPO experience+loss tokens/sec and % HBM roofline, 1/2/4/8 MI355X"
 METRIC_ILQL = "ILQL loss (fwd+bwd) action tokens/sec and % HBM roofline, MI355X (config 5, not the headline)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level table)
-TIMER_EVERY = 5        # instrument one step in five with per-kernel events
+TIMER_EVERY = 10       # instrument one step in ten: HIP events around the two vocab-row launches
 
 CONFIGS = {
     # name: (rows per GPU, response tokens, vocab, description)      BASELINE.json configs[]
@@ -44,8 +44,8 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--no-timers", action="store_true", help="skip per-kernel HIP events")
@@ -219,10 +219,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # Per-kernel HIP events on every TIMER_EVERY-th step of the timed region only: an
-    # event record between two kernels costs ~10 us of queue idle on this stack (measured),
-    # so instrumenting every step would tax the number it reports.
+    # Per-kernel HIP events on every TIMER_EVERY-th step of the timed region, around the
+    # vocab-row launches only (the roofline candidates): an event record between two
+    # kernels leaves the queue idle for microseconds on this stack (measured: a fully
+    # instrumented C2 step takes ~10% longer), so instrumenting more would tax `value`.
     timers = {}
+    hp.timer_names = {"rows"} if ilql else {"experience", "loss"}
     t0 = time.perf_counter()
     for i in range(args.steps):
         hp.timers = timers if (not args.no_timers and i % TIMER_EVERY == TIMER_EVERY - 1) else None

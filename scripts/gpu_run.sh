@@ -25,13 +25,13 @@ for step in "$@"; do
         sweep) run sweep 300 python tools/row_sweep.py ;;
         sweep_c4) B=128 T=128 V=32128 run sweep_c4 300 python tools/row_sweep.py ;;
         sweep_f32) DT=f32 run sweep_f32 300 python tools/row_sweep.py ;;
-        bench) run bench 400 python bench.py --steps 20 --warmup 5 ;;
-        bench_c3) run bench_c3 300 python bench.py --steps 20 --warmup 5 --config c3 --cpu-seconds 0 ;;
-        bench_c5) run bench_c5 300 python bench.py --steps 20 --warmup 5 --config c5 --cpu-seconds 10 ;;
+        bench) run bench 400 python bench.py ;;
+        bench_c3) run bench_c3 300 python bench.py --config c3 --cpu-seconds 0 ;;
+        bench_c5) run bench_c5 300 python bench.py --config c5 --cpu-seconds 10 ;;
         profile_c5) run profile_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 \
                      -o run -- python bench.py --steps 10 --warmup 3 --config c5 --cpu-seconds 0 --no-timers ;;
         ilql) run ilql_tests 300 python -u -m pytest tests/test_gpu_ilql.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-        bench_c4) run bench_c4 300 python bench.py --steps 20 --warmup 5 --config c4 --cpu-seconds 0 ;;
+        bench_c4) run bench_c4 300 python bench.py --config c4 --cpu-seconds 0 ;;
         profile_nt) run profile_nt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_nt \
                      -o run -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-timers ;;
         bench_nt) run bench_nt 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-timers ;;

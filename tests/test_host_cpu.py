@@ -105,7 +105,7 @@ def test_grad_buffer_phase(shape_stride):
         xv = full.view(-1)[off:off + x.numel()].view(x.shape) if kind is None else x
         d = P.grad_buffer_like(xv)
         assert d.shape == xv.shape and d.stride() == xv.stride()
-        assert (d.data_ptr() - xv.data_ptr()) % 16 == 0
+        assert (d.data_ptr() - xv.data_ptr()) % 256 == 0
 
 
 @pytest.mark.parametrize("world", [2])

@@ -144,7 +144,8 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
     const RowSplit<DT> s(x, a.V);
     const int nvec = int(s.nvec);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(x + s.head, uint32_t(nvec) * 16u);
-    const int voff = tid * 16;
+    const int shift = line_shift(x + s.head);  // whole 256-B spans per wave instruction (common.h)
+    const int voff = (tid - shift) * 16;
     vec4u v[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k)
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
         float mk = f[0];
 #pragma unroll
         for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
-        m = (tid + k * nthr < nvec) ? fmaxf(m, mk) : m;
+        m = (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? fmaxf(m, mk) : m;
     }
     m = block_max(m, sh_max);
 #pragma unroll
@@ -177,7 +178,7 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
         float sk = 0.0f;
 #pragma unroll
         for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
-        sum += (tid + k * nthr < nvec) ? sk : 0.0f;
+        sum += (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? sk : 0.0f;
     }
     sum = block_sum(sum, sh_sum);
 #pragma unroll
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
     const int iy = y_ok && y >= s.head && y < s.tail0 ? int((y - s.head) / EPV) : -1;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-        const int i = tid + k * nthr;  // lanes past the body: the store is range-checked away
+        const int i = tid - shift + k * nthr;  // lanes outside the body: range-checked away
         float f[EPV];
         DT::unpack(v[k], f);
 #pragma unroll
@@ -292,7 +293,7 @@ static const int kIlqlNVs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 16};
 // <= 1024 threads (fp32 V = 50257: 1024 threads x 13 vectors).
 static bool ilql_geometry(int64_t V, int elem_bytes, int& nv, int& threads) {
     const int epv = 16 / elem_bytes;
-    const int64_t nvec = V / epv + 1;
+    const int64_t nvec = V / epv + 1 + (kLineVecs - 1);
     for (int pref : {512, kMaxThreads}) {
         const int64_t need = (nvec + pref - 1) / pref;
         for (int c : kIlqlNVs) {

@@ -100,9 +100,9 @@ __device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row)
 
 // Forward epilogue: write lp (+lse).
 template <class DT>
-__device__ __forceinline__ void fwd_epilogue(const RowArgs& a, const Row<DT>& r, float lse) {
+__device__ __forceinline__ void fwd_epilogue(const RowArgs& a, const Row<DT>& r, float xy, float lse) {
     if (threadIdx.x == 0) {
-        const float lp = (r.y_ok ? DT::load1(r.x, r.y) : NAN) - lse;
+        const float lp = xy - lse;  // xy = x[y] (NaN for an out-of-range label), loaded early
         st_any(blockIdx.y == 0 ? a.lp0 : a.lp1, a.out_dtype, r.row, lp);
         float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
         if (lse_out) lse_out[r.row] = lse;
@@ -119,10 +119,12 @@ __device__ __forceinline__ float row_grad(const RowArgs& a, int64_t row, float l
     return g;
 }
 
-// After the row is stored (its registers dead): the token's loss record (fused loss).
+// After the row is stored (its registers dead): the token's loss record (fused loss);
+// vin = {values, old_values, returns} loaded in the prologue (loss_token_inputs).
 __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, const PolicyTerms& pt,
-                                             const PpoScalars& ps) {
-    if (a.tokrec && threadIdx.x == 0) loss_token_terms(a.ltok, a.tokrec, row, pt, ps.m, ps.inv_msum);
+                                             const PpoScalars& ps, const float* vin) {
+    if (a.tokrec && threadIdx.x == 0)
+        loss_token_terms(a.ltok, a.tokrec, row, pt, ps.m, ps.inv_msum, vin[0], vin[1], vin[2]);
 }
 
 // ------------------------------------------------------------------ register-resident rows
@@ -141,16 +143,20 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
     // Row-independent scalars first, computed by thread 0 while the row loads are in
     // flight and parked in LDS (read back after the reductions' barriers): they then
     // occupy no VGPRs beside the row.
-    __shared__ float s_ps[4];
+    __shared__ float s_ps[7];
     if (MODE == kPpo && tid == 0) {
         const PpoScalars p0 = ppo_scalars(a, r.row);
         s_ps[0] = p0.A; s_ps[1] = p0.m; s_ps[2] = p0.inv_msum; s_ps[3] = p0.olp;
+        if (a.tokrec) loss_token_inputs(a.ltok, r.row, s_ps + 4);
     }
 
     const int nvec = int(r.s.nvec);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(r.x + r.s.head, uint32_t(nvec) * 16u);
-    const int voff = tid * 16;  // + k*nthr*16 per vector, in VOFFSET: the raw-buffer range
-                                // check covers voffset (+imm), not soffset
+    const int shift = line_shift(r.x + r.s.head);  // whole 256-B spans per wave instruction
+    const int voff = (tid - shift) * 16;  // + k*nthr*16 per vector, in VOFFSET: the raw-buffer
+                                          // range check covers voffset (+imm), not soffset; the
+                                          // first `shift` lanes of k = 0 wrap to huge offsets
+                                          // and are dropped like the lanes past the body
     // ---- one HBM read of the row into registers (all loads in flight at once).  Vectors
     // past the row body read 0 (range check) and are excluded per vector below.
     vec4u v[NV];
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
             float mk = f[0];
 #pragma unroll
             for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
-            m = (tid + k * nthr < nvec) ? fmaxf(m, mk) : m;
+            m = (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? fmaxf(m, mk) : m;
         }
         m = block_max(m, sh_max);
 #pragma unroll
@@ -187,7 +193,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
             float sk = 0.0f;
 #pragma unroll
             for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
-            sum += (tid + k * nthr < nvec) ? sk : 0.0f;
+            sum += (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? sk : 0.0f;
         }
         sum = block_sum(sum, sh_sum);
 #pragma unroll
@@ -195,7 +201,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
         lse = m + logf(sum);
     }
     if (MODE == kFwd) {
-        fwd_epilogue(a, r, lse);
+        fwd_epilogue(a, r, xy, lse);
         return;
     }
 
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
         const int iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? int((r.y - r.s.head) / EPV) : -1;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const int i = tid + k * nthr;  // lanes past the body: the store is range-checked away
+            const int i = tid - shift + k * nthr;  // lanes outside the body: range-checked away
             float f[EPV];
             DT::unpack(v[k], f);
 #pragma unroll
@@ -237,8 +243,8 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
     } else {
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const int i = tid + k * nthr;
-            if (i < nvec) {
+            const int i = tid - shift + k * nthr;
+            if (unsigned(i) < unsigned(nvec)) {
                 float f[EPV];
                 DT::unpack(v[k], f);
 #pragma unroll
@@ -252,7 +258,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
     if (MODE == kPpo && tid == 0) {
         const PolicyTerms t2 = {s_tok[0], s_tok[1], s_tok[2], s_tok[3] != 0.f};
         const PpoScalars p2 = {0.f, s_tok[4], s_tok[5], 0.f};
-        token_record(a, r.row, t2, p2);
+        token_record(a, r.row, t2, p2, s_ps + 4);
     }
 }
 
@@ -335,11 +341,11 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
         for (int w = 1; w < nthr / kWave; ++w) online_merge(m, sum, sh_m[w], sh_s[w]);
         lse = m + logf(sum);
     }
+    const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
     if (MODE == kFwd) {
-        fwd_epilogue(a, r, lse);
+        fwd_epilogue(a, r, xy, lse);
         return;
     }
-    const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
     PolicyTerms pt = {1.f, 0.f, 0.f, false};
     const float g = row_grad<MODE>(a, r.row, xy - lse, ps, pt);
     const float lse_l2e = -lse * kLog2e;
@@ -381,7 +387,11 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
         }
     }
     if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
-    if (MODE == kPpo) token_record(a, r.row, pt, ps);
+    if (MODE == kPpo && a.tokrec && tid == 0) {
+        float vin[3];
+        loss_token_inputs(a.ltok, r.row, vin);
+        token_record(a, r.row, pt, ps, vin);
+    }
 }
 
 // ------------------------------------------------------------------ launch geometry
@@ -406,7 +416,7 @@ static const int kNVs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 16};
 
 static Geometry pick_geometry(int64_t V, int elem_bytes, bool allow_1024) {
     const int epv = 16 / elem_bytes;
-    const int64_t nvec = V / epv + 1;  // upper bound incl. head/tail peeling
+    const int64_t nvec = V / epv + 1 + (kLineVecs - 1);  // upper bound incl. peeling and line shift
     const int prefs[2] = {g_resident_threads > 0 ? g_resident_threads : 512, kMaxThreads};
     for (int pi = 0; pi < (allow_1024 ? 2 : 1); ++pi) {
         const int pref = prefs[pi];

@@ -198,9 +198,10 @@ class ILQLHotPath:
         self.dlogits = None
         self.dq = None
         self.timers = None  # optional {name: [[start_event, end_event], ...]}
+        self.timer_names = None  # optional subset of launch names to instrument (None = all)
 
     def _timed(self, name, s, fn):
-        if self.timers is None:
+        if self.timers is None or (self.timer_names is not None and name not in self.timer_names):
             return fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)

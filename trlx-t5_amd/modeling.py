@@ -106,13 +106,15 @@ def _token_geometry(logits: torch.Tensor, labels: torch.Tensor):
 
 
 def grad_buffer_like(x: torch.Tensor) -> torch.Tensor:
-    """Uninitialised tensor with x's size/strides whose rows have x's 16-byte phase, so the
-    kernels can write dlogits with the same aligned 16-B vectors they read logits with."""
+    """Uninitialised tensor with x's size/strides whose rows have x's 256-byte phase, so the
+    kernels write dlogits with the same 16-B vectors, grouped into the same whole 256-B
+    spans, that they read logits with (the kernels need the 16-B phase for correctness;
+    the 256-B phase keeps the stores line-aligned, common.h line_shift)."""
     es = x.element_size()
     extent = 1 + sum((s - 1) * st for s, st in zip(x.shape, x.stride()) if s > 0)
-    pad = 16 // es
+    pad = 256 // es
     buf = torch.empty(extent + pad, dtype=x.dtype, device=x.device)
-    off = ((x.data_ptr() - buf.data_ptr()) % 16) // es
+    off = ((x.data_ptr() - buf.data_ptr()) % 256) // es
     return buf.as_strided(x.shape, x.stride(), off)
 
 

@@ -56,10 +56,11 @@ class PPOHotPath:
         self.workspace = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)  # tickets re-armed in-kernel
         self.dlogits = None
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
+        self.timer_names = None  # optional subset of launch names to instrument (None = all)
 
     # -------------------------------------------------------------- helpers
     def _ev(self, name, s):
-        if self.timers is None:
+        if self.timers is None or (self.timer_names is not None and name not in self.timer_names):
             return None
         e = torch.cuda.Event(enable_timing=True)
         e.record(s)
@@ -67,7 +68,7 @@ class PPOHotPath:
         return e
 
     def _ev_end(self, name, s):
-        if self.timers is None:
+        if self.timers is None or (self.timer_names is not None and name not in self.timer_names):
             return
         e = torch.cuda.Event(enable_timing=True)
         e.record(s)
