@@ -14,7 +14,7 @@ all-reduce between the two halves):
                                            dlogits (V*s read + V*s write / token), d values,
                                            per-token loss terms (ppo_models.py:141-199)
               trlx_ppo_rollout_loss        fixed-order loss sums -> loss + 13 stats
-      [RCCL all-reduce of the stats vector for logging when world > 1]
+      [optional RCCL all-reduce of the stats vector for logging (reduce_stats=True)]
 
 Buffers (and the zero-filled ticket workspace) are allocated once per shape; a step
 allocates nothing.  Rows (rollouts) are sharded contiguously across ranks by the caller
@@ -132,7 +132,10 @@ class PPOHotPath:
 
     def step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
              lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None,
-             reduce_stats: bool = True):
+             reduce_stats: bool = False):
+        """One experience + loss pass over this rank's shard.  The loss stats are rank-local
+        like the reference's (ppo_models.py:162-198 runs per rank; Accelerate logs rank 0);
+        reduce_stats=True averages them over ranks with one extra all-reduce (logging)."""
         for t in (labels, old_values, values, scores):
             if not t.is_contiguous():
                 raise ValueError("labels / values / scores must be contiguous")
