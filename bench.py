@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--no-timers", action="store_true", help="skip per-kernel HIP events")
+    p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                   help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                        "several ranks on one GPU)")
     return p.parse_args()
 
 
@@ -191,10 +194,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     B, T, V, desc = CONFIGS[args.config]
     ilql = args.config == "c5"

@@ -27,3 +27,26 @@ def whiten_stats_worker(rank, world, port, xs, q):
     q.put((rank, float(mean), float(var), float(st[2])))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def hot_path_step_worker(rank, world, port, inputs, q):
+    """One rank of a DP PPO step on cuda:0 over gloo (the product's exchange: the whitening
+    record all-reduce inside PPOHotPath.experience).  Rank r takes the contiguous row block
+    r of the batch (accelerate_ppo_model.py:146-148 sharding)."""
+    import torch.distributed as dist
+    import trlx_t5_amd as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    sh = {k: (v.chunk(world, dim=0)[rank].contiguous().to(dev) if v is not None else None) for k, v in inputs.items()}
+    B, T, V = sh["logits"].shape
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05)
+    loss, stats, dlogits, dvalues = hp.step(sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"],
+                                            sh["old_values"], sh["values"], sh["scores"], lengths=sh["lengths"],
+                                            mask=sh["mask"])
+    torch.cuda.synchronize()
+    q.put((rank, {"lp": hp.lp_old.cpu(), "rewards": hp.rewards.cpu(), "adv_stats": hp.adv_stats.cpu(),
+                  "loss": loss.cpu(), "dlogits": dlogits.float().cpu(), "dvalues": dvalues.cpu(),
+                  "stats": stats.cpu()}))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,0 +1,77 @@
+"""Data-parallel PPO step on the GPU with world size 2 (two processes sharing cuda:0, gloo
+process group — the 8-GPU RCCL run is the driver's; this checks the sharded semantics):
+every rank streams only its row block, the whitening statistics are the GLOBAL biased
+moments (modeling.py:9-21 branch of whiten, one all-reduce of {Σ A, Σ A², n}), and each
+rank's loss / gradients match the oracle applied to its shard with the global whitening
+(loss normalisers rank-local, ppo_models.py:162,177)."""
+import os
+
+import pytest
+import torch
+
+from oracle import ppo_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(B, T, V, seed, lengths):
+    g = torch.Generator().manual_seed(seed)
+    logits = torch.randn(B, T, V, generator=g).to(torch.bfloat16)
+    ref_logits = (logits.float() + 0.1 * torch.randn(B, T, V, generator=g)).to(torch.bfloat16)
+    new_logits = (logits.float() + 0.05 * torch.randn(B, T, V, generator=g)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, T), generator=g)
+    old_values = torch.randn(B, T, generator=g)
+    values = old_values + 0.3 * torch.randn(B, T, generator=g)
+    scores = torch.rand(B, generator=g) * 24 - 12
+    L = mask = None
+    if lengths:
+        L = torch.randint(1, T + 1, (B,), generator=g)
+        mask = (torch.arange(T)[None, :] < L[:, None]).long()
+        old_values = old_values.masked_fill(mask == 0, 0)
+    return dict(logits=logits, ref_logits=ref_logits, new_logits=new_logits, labels=labels, old_values=old_values,
+                values=values, scores=scores, lengths=L, mask=mask)
+
+
+@pytest.mark.parametrize("lengths", [False, True])
+def test_dp2_step_global_whitening(lengths):
+    import torch.multiprocessing as mp
+    import dist_workers
+    world, B, T, V = 2, 8, 20, 1031
+    x = _inputs(B, T, V, 5 + lengths, lengths)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 300
+    ps = [ctx.Process(target=dist_workers.hot_path_step_worker, args=(r, world, port, x, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    # oracle: experience per row, GAE per row, whitening with the GLOBAL biased moments
+    f = {k: (v.float() if v is not None and v.is_floating_point() else v) for k, v in x.items()}
+    lp = orc.logprobs_from_logits(f["logits"], x["labels"])
+    ref_lp = orc.logprobs_from_logits(f["ref_logits"], x["labels"])
+    rewards = orc.kl_penalty_rewards(lp, ref_lp, 0.05, x["scores"], x["lengths"])
+    adv, ret = orc.gae(x["old_values"], rewards, T, 1.0, 0.95, use_whitening=False)
+    mu = adv.double().mean()
+    var = ((adv.double() - mu) ** 2).mean()
+    advw = ((adv.double() - mu) * torch.rsqrt(var + 1e-8)).float()
+    for r in range(world):
+        got = res[r]
+        rows = slice(r * B // world, (r + 1) * B // world)
+        torch.testing.assert_close(got["lp"], lp[rows], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(got["rewards"], rewards[rows], rtol=1e-5, atol=1e-5)
+        st = got["adv_stats"]
+        assert float(st[2]) == B * T  # the all-reduced count covers both shards
+        torch.testing.assert_close(st[0], adv.double().sum(), rtol=1e-5, atol=1e-5)
+        xg = f["new_logits"][rows].clone().requires_grad_(True)
+        vg = x["values"][rows].clone().requires_grad_(True)
+        new_lp = orc.logprobs_from_logits(xg, x["labels"][rows])
+        m = torch.ones(B // world, T, dtype=torch.long) if x["mask"] is None else x["mask"][rows]
+        loss, _ = orc.ppo_loss(new_lp, vg, lp[rows], x["old_values"][rows], advw[rows], ret[rows], m)
+        loss.backward()
+        torch.testing.assert_close(got["loss"].reshape(()), loss.detach(), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(got["dlogits"], xg.grad, rtol=2e-2, atol=1e-6)
+        torch.testing.assert_close(got["dvalues"], vg.grad, rtol=1e-5, atol=1e-6)
