@@ -37,6 +37,10 @@ for step in "$@"; do
         bench_nt) run bench_nt 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-timers ;;
         profile) run profile 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
                      -o run -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+        pmc_fetch_c5) run pmc_fetch_c5 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_c5 \
+                     -o run -- python bench.py --steps 3 --warmup 1 --config c5 --cpu-seconds 0 --no-timers ;;
+        pmc_write_c5) run pmc_write_c5 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_c5 \
+                     -o run -- python bench.py --steps 3 --warmup 1 --config c5 --cpu-seconds 0 --no-timers ;;
         pmc_fetch) run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch \
                      -o run -- python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-timers ;;
         pmc_write) run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write \

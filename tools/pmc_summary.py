@@ -37,6 +37,12 @@ def kernel_key(name):
         return "rollout_gae"
     if "k_rollout_loss" in name:
         return "rollout_loss"
+    if "k_ilql_rows" in name:
+        return "rows"
+    if "k_ilql_prep" in name:
+        return "prep"
+    if "k_ilql_finalize" in name:
+        return "finalize"
     return None
 
 
