@@ -61,9 +61,10 @@ const char* trlx_last_error(void);
 /* Process-wide launch tuning (0 = automatic, the default).  Keys:
  *   "row_variant"       1 = register-resident vocab rows, 2 = streaming vocab rows
  *   "resident_threads"  workgroup size for resident rows (multiple of 64)
- *   "resident_lb512"    1 (default) = <=512-thread resident rows compiled for 6 waves/SIMD
+ *   "resident_lb512"    1 = <=512-thread resident rows compiled for 6 waves/SIMD (default 0)
  *   "stream_threads"    workgroup size for streaming rows
  *   "stream_unroll"     16-B loads in flight per thread for streaming rows (2, 4, 8)
+ *   "row_order"         resident rows: 0 (default) = step-major vectors, 1 = wave-major
  * Results are identical up to fp32 summation order; only speed changes. */
 int trlx_set_tuning(const char* key, int64_t value);
 

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
     const int nvec = int(s.nvec);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(x + s.head, uint32_t(nvec) * 16u);
     const int shift = line_shift(x + s.head);  // whole 256-B spans per wave instruction (common.h)
-    const int voff = (tid - shift) * 16;
+    const int voff = (tid - shift) * 16;       // step-major vector order (vocab_rows.hip)
     vec4u v[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k)

@@ -40,6 +40,7 @@ struct RowArgs {
     const float* adv;
     const double* stats;
     int unbiased;
+    int order;                // vector order of the resident rows (0 step-major, 1 wave-major)
     const int64_t* mask;
     const double* msum;
     double msum_host;
@@ -153,16 +154,20 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
     const int nvec = int(r.s.nvec);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(r.x + r.s.head, uint32_t(nvec) * 16u);
     const int shift = line_shift(r.x + r.s.head);  // whole 256-B spans per wave instruction
-    const int voff = (tid - shift) * 16;  // + k*nthr*16 per vector, in VOFFSET: the raw-buffer
-                                          // range check covers voffset (+imm), not soffset; the
-                                          // first `shift` lanes of k = 0 wrap to huge offsets
-                                          // and are dropped like the lanes past the body
+    // Vector order (tuning "row_order"): 0 = step-major (vector tid + k*nthr), 1 = wave-major
+    // (wave w owns the contiguous vectors [w*NV*64, (w+1)*NV*64)); both issue one 1-KB span
+    // per wave instruction.  Both strides are runtime values, so the per-vector offsets are
+    // added in VOFFSET (the raw-buffer range check covers voffset + imm, not soffset): the
+    // first `shift` lanes wrap to huge offsets at k = 0 and are dropped like those past the body.
+    const int vbase = (a.order ? (tid >> 6) * (NV * kWave) + (tid & (kWave - 1)) : tid) - shift;
+    const int vstep = a.order ? kWave : nthr;
+    const int voff = vbase * 16;
     // ---- one HBM read of the row into registers (all loads in flight at once).  Vectors
     // past the row body read 0 (range check) and are excluded per vector below.
     vec4u v[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-        v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, launder_int(voff) + k * nthr * 16, 0, kAuxNT);
+        v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, launder_int(voff) + k * vstep * 16, 0, kAuxNT);
     const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
     const int64_t je = r.edge_index();
     const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
             float mk = f[0];
 #pragma unroll
             for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
-            m = (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? fmaxf(m, mk) : m;
+            m = (unsigned(vbase + k * vstep) < unsigned(nvec)) ? fmaxf(m, mk) : m;
         }
         m = block_max(m, sh_max);
 #pragma unroll
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
             float sk = 0.0f;
 #pragma unroll
             for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
-            sum += (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? sk : 0.0f;
+            sum += (unsigned(vbase + k * vstep) < unsigned(nvec)) ? sk : 0.0f;
         }
         sum = block_sum(sum, sh_sum);
 #pragma unroll
@@ -227,7 +232,7 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
         const int iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? int((r.y - r.s.head) / EPV) : -1;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const int i = tid - shift + k * nthr;  // lanes outside the body: range-checked away
+            const int i = vbase + k * vstep;  // lanes outside the body: range-checked away
             float f[EPV];
             DT::unpack(v[k], f);
 #pragma unroll
@@ -238,12 +243,12 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
                 for (int e = 0; e < EPV; ++e)
                     if (e == ey) f[e] = gy;
             }
-            __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, launder_int(voff) + k * nthr * 16, 0, kAuxNT);
+            __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, launder_int(voff) + k * vstep * 16, 0, kAuxNT);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-            const int i = tid - shift + k * nthr;
+            const int i = vbase + k * vstep;
             if (unsigned(i) < unsigned(nvec)) {
                 float f[EPV];
                 DT::unpack(v[k], f);
@@ -406,6 +411,7 @@ static int g_resident_threads = 0;  // preferred workgroup size for resident row
 static int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 6 waves/SIMD
 static int g_stream_threads = 0;
 static int g_stream_unroll = 0;
+static int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
 // workgroup size.  Default: 512-thread workgroups (8 waves) -- measured on MI355X (C2,
@@ -441,7 +447,9 @@ static bool rows_same_phase(const RowArgs& a, size_t es) {
 }
 
 template <int MODE, class DT>
-static int launch_rows_dt(const RowArgs& a, int nten, hipStream_t stream) {
+static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
+    RowArgs a = a0;
+    a.order = g_row_order;
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
@@ -669,6 +677,9 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
         TRLX_REQUIRE(value == 0 || (value % kWave == 0 && value <= kStreamMaxThreads), TRLX_ERR_ARG,
                      "stream_threads must be a multiple of 64 <= %d", kStreamMaxThreads);
         g_stream_threads = int(value);
+    } else if (k == "row_order") {
+        TRLX_REQUIRE(value == 0 || value == 1, TRLX_ERR_ARG, "row_order: 0 or 1");
+        g_row_order = int(value);
     } else if (k == "stream_unroll") {
         TRLX_REQUIRE(value == 0 || value == 2 || value == 4 || value == 8, TRLX_ERR_ARG, "stream_unroll: 2, 4 or 8");
         g_stream_unroll = int(value);

@@ -17,6 +17,7 @@ import torch
 
 from . import _lib
 from .modeling import grad_buffer_like
+from .timing import make_event
 
 __all__ = ["ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS"]
 
@@ -203,7 +204,7 @@ class ILQLHotPath:
     def _timed(self, name, s, fn):
         if self.timers is None or (self.timer_names is not None and name not in self.timer_names):
             return fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0, e1 = make_event(), make_event()
         e0.record(s)
         fn()
         e1.record(s)

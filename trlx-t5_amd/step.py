@@ -29,6 +29,7 @@ import torch.distributed as dist
 from . import _lib
 from .modeling import grad_buffer_like
 from .ppo import PPOConfig
+from .timing import make_event
 
 __all__ = ["PPOHotPath"]
 
@@ -62,7 +63,7 @@ class PPOHotPath:
     def _ev(self, name, s):
         if self.timers is None or (self.timer_names is not None and name not in self.timer_names):
             return None
-        e = torch.cuda.Event(enable_timing=True)
+        e = make_event()
         e.record(s)
         self.timers.setdefault(name, []).append([e, None])
         return e
@@ -70,7 +71,7 @@ class PPOHotPath:
     def _ev_end(self, name, s):
         if self.timers is None or (self.timer_names is not None and name not in self.timer_names):
             return
-        e = torch.cuda.Event(enable_timing=True)
+        e = make_event()
         e.record(s)
         self.timers[name][-1][1] = e
 
