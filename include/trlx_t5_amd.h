@@ -276,6 +276,20 @@ int trlx_ilql_rows(const trlx_ilql_args* args, void* stream);
 int trlx_ilql_finalize(const trlx_ilql_args* args, void* stream);
 int trlx_ilql_loss_fused(const trlx_ilql_args* args, void* stream);   /* the three in order */
 
+/* ---------------------------------------------------------------- §8f: device-resident rollout store
+ * Row copy between padded columnar [rows, W] buffers — replaces the reference's
+ * `.cpu()` of the experience tensors, per-sample PPORLElement lists and the pad_sequence
+ * collate (ppo_orchestrator.py:169-187, ppo_pipeline.py:36-66).  For each of nfields
+ * (<= 8) fields i, for j < rows and c < cols[i]:
+ *   dst[i][drow(j) * dst_ld[i] + dst_col0[i] + c] = src[i][srow(j) * src_ld[i] + src_col0[i] + c]
+ * srow(j) = src_idx ? src_idx[j] : src_row0 + j (drow likewise); element size esize[i] in
+ * {2, 4, 8} bytes; strides / columns in elements.  The host arrays are read during the call
+ * only; src_idx / dst_idx are device int64 vectors. */
+int trlx_rows_copy(int nfields, const void* const* src, void* const* dst, const int64_t* src_ld,
+                   const int64_t* dst_ld, const int64_t* src_col0, const int64_t* dst_col0,
+                   const int64_t* cols, const int* esize, int64_t rows, const int64_t* src_idx,
+                   int64_t src_row0, const int64_t* dst_idx, int64_t dst_row0, void* stream);
+
 /* ---------------------------------------------------------------- autograd plumbing
  * out[i] = x[i] * (*scale) for i < n (scale: device fp32 scalar, e.g. a backward's
  * grad_output).  In place (out == x) it is skipped entirely when *scale == 1. */

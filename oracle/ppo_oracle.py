@@ -240,3 +240,18 @@ def ilql_loss(logits, qs, target_qs, vs, input_ids, attention_mask, rewards, act
     stats = {"losses/loss": loss, "losses/loss_q": loss_q, "losses/loss_v": loss_v,
              "losses/loss_cql": loss_cql, "losses/loss_awac": loss_awac}
     return loss, stats
+
+
+# ------------------------------------------------------------------ trlx/pipeline/ppo_pipeline.py
+def ppo_collate(elems, pad_token_id):
+    """ppo_pipeline.py:40-66 — queries left-padded (flip, pad_sequence, flip), the rest
+    right-padded (tokens with pad_token_id, floats with 0.0).  elems: objects with
+    query_tensor, response_tensor, logprobs, values, rewards."""
+    from torch.nn.utils.rnn import pad_sequence
+    return (
+        pad_sequence([e.query_tensor.flip(0) for e in elems], padding_value=pad_token_id, batch_first=True).flip(1),
+        pad_sequence([e.response_tensor for e in elems], padding_value=pad_token_id, batch_first=True),
+        pad_sequence([e.logprobs for e in elems], padding_value=0.0, batch_first=True),
+        pad_sequence([e.values for e in elems], padding_value=0.0, batch_first=True),
+        pad_sequence([e.rewards for e in elems], padding_value=0.0, batch_first=True),
+    )

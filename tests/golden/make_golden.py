@@ -421,16 +421,65 @@ def make_ilql(ilql_models, ilql_types):
     np.savez_compressed(os.path.join(OUT, "ilql_loss.npz"), **out)
 
 
+# --------------------------------------------------------------------------- §8f rollout store
+def load_ppo_pipeline():
+    """trlx/pipeline/ppo_pipeline.py with its real package deps (trlx.data, trlx.pipeline)."""
+    sys.modules.pop("trlx.data", None)
+    d = _load("trlx.data", "trlx/data/__init__.py")
+    d.__path__ = []
+    _load("trlx.data.method_configs", "trlx/data/method_configs.py")
+    types_mod = _load("trlx.data.ppo_types", "trlx/data/ppo_types.py")
+    p = _load("trlx.pipeline", "trlx/pipeline/__init__.py")
+    p.__path__ = []
+    return _load("trlx.pipeline.ppo_pipeline", "trlx/pipeline/ppo_pipeline.py"), types_mod
+
+
+def make_rollout_store(ppo_pipeline, ppo_types):
+    """PPORolloutStorage.push + create_loader(shuffle=False) over three experience chunks
+    of different query / response widths (the reference's own collate, ppo_pipeline.py)."""
+    out = {}
+    g = gen(700)
+    store = ppo_pipeline.PPORolloutStorage(pad_token_id=0)
+    store.clear_history()  # the reference constructs history = [None] and clears it before use
+    chunks = [(3, 5, 4), (4, 7, 6), (2, 3, 2)]  # (rows, query width, response width)
+    for ci, (n, wq, wr) in enumerate(chunks):
+        q = torch.randint(1, 50, (n, wq), generator=g)
+        q[0, :2] = 0  # the chunk's own left padding
+        r = torch.randint(1, 50, (n, wr), generator=g)
+        r[-1, -1] = 0
+        lp, v, rw = (torch.randn(n, wr, generator=g) for _ in range(3))
+        elems = [ppo_types.PPORLElement(q[i], r[i], lp[i], v[i], rw[i]) for i in range(n)]
+        store.push(elems)
+        for name, t in (("query", q), ("response", r), ("logprobs", lp), ("values", v), ("rewards", rw)):
+            out[f"chunk{ci}/{name}"] = t.numpy()
+    loader = store.create_loader(4, shuffle=False)
+    for bi, batch in enumerate(loader):
+        for name in ("query_tensors", "response_tensors", "logprobs", "values", "rewards"):
+            out[f"batch{bi}/{name}"] = getattr(batch, name).numpy()
+    out["n_batches"] = np.array(bi + 1)
+    np.savez_compressed(os.path.join(OUT, "rollout_store.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(4)
+    only = sys.argv[1:]
     modeling, ppo_models, ilql_models, ilql_types = load_reference()
-    make_lsm_gather(modeling)
-    make_kl_reward(modeling)
-    make_gae(ppo_models)
-    make_ppo_loss(ppo_models, modeling)
-    make_host_state(modeling, ppo_models)
-    make_ilql(ilql_models, ilql_types)
-    make_whiten(modeling)
+    if not only or "lsm" in only:
+        make_lsm_gather(modeling)
+    if not only or "kl" in only:
+        make_kl_reward(modeling)
+    if not only or "gae" in only:
+        make_gae(ppo_models)
+    if not only or "loss" in only:
+        make_ppo_loss(ppo_models, modeling)
+    if not only or "host" in only:
+        make_host_state(modeling, ppo_models)
+    if not only or "ilql" in only:
+        make_ilql(ilql_models, ilql_types)
+    if not only or "whiten" in only:
+        make_whiten(modeling)
+    if not only or "store" in only:
+        make_rollout_store(*load_ppo_pipeline())
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
