@@ -276,6 +276,21 @@ int trlx_ilql_rows(const trlx_ilql_args* args, void* stream);
 int trlx_ilql_finalize(const trlx_ilql_args* args, void* stream);
 int trlx_ilql_loss_fused(const trlx_ilql_args* args, void* stream);   /* the three in order */
 
+/* ---------------------------------------------------------------- §8f rank 2: fused lm_head + logprobs
+ * lp[n] = h[n]·W[y_n] − logsumexp_v h[n]·W[v] without materialising the [N, V] logits —
+ * replaces `logits = lm_head(hs)` (ppo_models.py:640 T5HeadWithValueModel, :274/:588 GPT)
+ * + logprobs_from_logits (modeling.py:37-41) on the experience side
+ * (ppo_orchestrator.py:135-155, no gradient).  hidden: bf16 [N, H] rows of ldh elements;
+ * weight: bf16 [V, H] (nn.Linear layout) rows of ldw; H a multiple of 64, rows 16-B
+ * aligned.  labels int64 (stride lb; out of range -> NaN).  lp_out [N] of lp_dtype
+ * (F32/BF16), lse_out optional fp32 [N].  MFMA (bf16 in, fp32 accumulate) tiles of
+ * 128 tokens x 128 vocab with an online max/Σexp epilogue, then a per-token combine.
+ * workspace: trlx_lmhead_workspace_bytes(N, V) bytes (no initialisation needed). */
+int64_t trlx_lmhead_workspace_bytes(int64_t N, int64_t V);
+int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
+                         int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
+                         int lp_dtype, float* lse_out, void* workspace, void* stream);
+
 /* ---------------------------------------------------------------- §8f: device-resident rollout store
  * Row copy between padded columnar [rows, W] buffers — replaces the reference's
  * `.cpu()` of the experience tensors, per-sample PPORLElement lists and the pad_sequence

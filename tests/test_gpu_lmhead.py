@@ -1,0 +1,84 @@
+"""Fused lm_head + logprobs (csrc/lmhead_rows.hip) through the C ABI,
+against the oracle path it replaces: logprobs_from_logits(hidden @ weight.T, labels)
+(modeling.py:37-41, oracle/ppo_oracle.py) evaluated in fp64 on the same bf16 inputs.
+
+Tolerance: the kernel multiplies bf16 inputs exactly and accumulates in fp32 (MFMA), so the
+logits differ from fp64 by summation order only (~1e-7 relative); logprobs are compared at
+rtol 1e-5 + atol 1e-4 (fp32 output) and at bf16 resolution (rtol 1e-2) for bf16 output.
+Label gathers are exact: out-of-range labels give NaN, never an out-of-bounds read."""
+import pytest
+import torch
+
+import trlx_t5_amd as P
+from oracle import ppo_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def oracle_lp(h, w, y):
+    logits = h.double() @ w.double().t()
+    yy = y.clamp(0, w.shape[0] - 1)
+    lp = orc.logprobs_from_logits(logits, yy)
+    return torch.where((y >= 0) & (y < w.shape[0]), lp, torch.full_like(lp, float("nan")))
+
+
+def case(N, H, V, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    h = (torch.randn(N, H, generator=g) * scale).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * scale).to(torch.bfloat16)
+    y = torch.randint(0, V, (N,), generator=g)
+    y[0] = 0
+    y[-1] = V - 1
+    return h, w, y
+
+
+@pytest.mark.parametrize("N,H,V,scale", [
+    (1, 64, 23, 1.0), (5, 128, 128, 1.0), (130, 64, 129, 1.0), (257, 768, 1031, 0.1), (64, 768, 50257, 0.2),
+    (200, 256, 32128, 0.3), (129, 4096, 384, 0.05),
+])
+def test_lmhead_vs_oracle(N, H, V, scale):
+    h, w, y = case(N, H, V, N + H + V, scale)
+    lp, lse = P.lm_head_logprobs(h.to(DEV), w.to(DEV), y.to(DEV), out_dtype=torch.float32, return_lse=True)
+    want = oracle_lp(h, w, y)
+    torch.testing.assert_close(lp.cpu().double(), want, rtol=1e-5, atol=1e-4)
+    want_lse = torch.logsumexp(h.double() @ w.double().t(), -1)
+    torch.testing.assert_close(lse.cpu().double(), want_lse, rtol=1e-5, atol=1e-4)
+
+
+def test_lmhead_bf16_out_strided_and_bad_labels():
+    """bf16 output (the reference's logits dtype), a [B, T, H] view whose rows are strided
+    (a causal hs[:, :-1] slice), and labels outside [0, V) -> NaN."""
+    B, T, H, V = 3, 9, 128, 1000
+    g = torch.Generator().manual_seed(4)
+    full = (torch.randn(B, T + 1, H, generator=g) * 0.3).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * 0.3).to(torch.bfloat16)
+    y = torch.randint(0, V, (B, T), generator=g)
+    y[1, 2] = V
+    y[2, 0] = -1
+    hd = full.to(DEV)[:, :-1]
+    assert not hd.is_contiguous()
+    lp = P.lm_head_logprobs(hd, w.to(DEV), y.to(DEV))
+    assert lp.dtype == torch.bfloat16 and lp.shape == (B, T)
+    want = oracle_lp(full[:, :-1].reshape(-1, H), w, y.reshape(-1)).view(B, T)
+    got = lp.cpu().float().double()
+    assert torch.isnan(got[1, 2]) and torch.isnan(got[2, 0])
+    ok = ~torch.isnan(want)
+    torch.testing.assert_close(got[ok], want[ok], rtol=1e-2, atol=1e-2)
+
+
+def test_lmhead_c2_shape_rows_and_determinism():
+    """The C2 experience shape (6144 tokens, H 768, V 50257): a row sample against the fp64
+    oracle, bitwise-identical repeats."""
+    N, H, V = 6144, 768, 50257
+    g = torch.Generator(device=DEV).manual_seed(7)
+    h = (torch.randn(N, H, generator=g, device=DEV) * 0.15).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g, device=DEV) * 0.15).to(torch.bfloat16)
+    y = torch.randint(0, V, (N,), generator=g, device=DEV)
+    lp1 = P.lm_head_logprobs(h, w, y, out_dtype=torch.float32)
+    lp2 = P.lm_head_logprobs(h, w, y, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(lp1, lp2)
+    rows = torch.tensor([0, 1, 127, 128, 2047, 4096, 6000, 6143])
+    want = oracle_lp(h[rows.to(DEV)].cpu(), w.cpu(), y[rows.to(DEV)].cpu())
+    torch.testing.assert_close(lp1[rows.to(DEV)].cpu().double(), want, rtol=1e-5, atol=1e-4)

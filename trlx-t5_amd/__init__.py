@@ -10,6 +10,7 @@ Drop-in names (reference file:line in danyang-rainbow/trlx-t5):
       trlx/orchestrator/ppo_orchestrator.py:96-112,163-167
   ILQLConfig (.loss), ILQLBatch
       trlx/model/nn/ilql_models.py:52-116, trlx/data/ilql_types.py
+  lm_head_logprobs — fused lm_head GEMM (MFMA) + logprobs, logits never in HBM
   PPORolloutStorage, PPORLElement, PPORLBatch
       trlx/pipeline/ppo_pipeline.py, trlx/data/ppo_types.py (device-resident store)
   PPOHotPath — the fused device-resident experience+loss step (bench / DP shard)
@@ -22,6 +23,7 @@ from .modeling import (RunningMoments, flatten_dict, get_global_statistics, grad
                        logprobs_from_logits, moments, whiten)
 from .ppo import (STATS_KEYS, AdaptiveKLController, FixedKLController, PPOConfig, kl_penalty_rewards,
                   prepare_scores, stats_dict)
+from .lm_head import lm_head_logprobs
 from .rollout_store import PPORLBatch, PPORLElement, PPORolloutStorage
 from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig, ILQLHotPath
 from .step import PPOHotPath
@@ -31,6 +33,7 @@ __all__ = [
     "grad_buffer_like", "PPOConfig", "AdaptiveKLController", "FixedKLController", "kl_penalty_rewards",
     "prepare_scores", "stats_dict", "STATS_KEYS", "PPOHotPath", "load_library",
     "ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS", "PPORolloutStorage", "PPORLElement", "PPORLBatch",
+    "lm_head_logprobs",
 ]
 
 

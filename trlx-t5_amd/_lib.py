@@ -88,6 +88,9 @@ SIGNATURES = {
                                      _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                                      _c_vp, _c_int, _c_vp, _c_int, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_i64,
                                      _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "trlx_lmhead_workspace_bytes": (_c_i64, [_c_i64, _c_i64]),
+    "trlx_lmhead_logprobs": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp,
+                                      _c_int, _c_vp, _c_vp, _c_vp]),
     "trlx_rows_copy": (_c_int, [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp,
                                 _c_i64, _c_vp, _c_i64, _c_vp]),
     "trlx_ilql_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_int]),
