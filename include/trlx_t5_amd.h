@@ -287,6 +287,11 @@ int trlx_ilql_loss_fused(const trlx_ilql_args* args, void* stream);   /* the thr
  * 128 tokens x 128 vocab with an online max/Σexp epilogue, then a per-token combine.
  * workspace: trlx_lmhead_workspace_bytes(N, V) bytes (no initialisation needed). */
 int64_t trlx_lmhead_workspace_bytes(int64_t N, int64_t V);
+/* Kernel variant (0 = automatic: 256x256 tiles for N >= 2048, else 128x128; 1 persistent
+ * 256x256 with 3 stages in flight; 2 256x256 tiles; 3 128x128 tiles; 4 = 2 with an XCD-aware
+ * tile order).  Results identical up to fp32 summation order.  Set before sizing the
+ * workspace (the vocab tile width changes it). */
+int trlx_lmhead_set_variant(int variant);
 int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                          int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
                          int lp_dtype, float* lse_out, void* workspace, void* stream);

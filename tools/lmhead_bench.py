@@ -36,7 +36,13 @@ def main():
         h = (torch.randn(N, H, generator=g, device=dev) * 0.1).to(torch.bfloat16)
         w = (torch.randn(V, H, generator=g, device=dev) * 0.1).to(torch.bfloat16)
         y = torch.randint(0, V, (N,), generator=g, device=dev)
-        fused = timeit(lambda: P.lm_head_logprobs(h, w, y, out_dtype=torch.float32))
+        res = {}
+        for var in (2, 4, 1):
+            P._lib.call("trlx_lmhead_set_variant", var)
+            res[var] = timeit(lambda: P.lm_head_logprobs(h, w, y, out_dtype=torch.float32))
+        P._lib.call("trlx_lmhead_set_variant", 0)
+        fused = min(res.values())
+        print("   variants (us):", {k: round(v, 1) for k, v in res.items()})
         gemm = timeit(lambda: h @ w.t())
         logits = h @ w.t()
         rows = timeit(lambda: P.logprobs_from_logits(logits, y))

@@ -7,12 +7,12 @@
 // :588) followed by logprobs_from_logits (modeling.py:37-41) on the experience side
 // (ppo_orchestrator.py:135-155), where no gradient is needed.  Two launches:
 //
-//   k_lmhead_tiles    MFMA GEMM over 128 tokens x 128 vocab tiles (K = H streamed in 64-deep
+//   k_lmhead_tiles    MFMA GEMM over 256 x 256 (or 128 x 128) token x vocab tiles (K = H in 64-deep
 //                     steps through double-buffered LDS by global_load_lds, 16 B per lane, an
 //                     XOR-swizzled image read conflict-free with ds_read_b128); the epilogue
 //                     reduces each token's 128 logits of the tile to a partial (max, Σexp)
 //                     and the tile that holds the label stores its logit.
-//   k_lmhead_combine  one wave per token merges its V/128 partials -> lse, lp = x_y − lse.
+//   k_lmhead_combine  one wave per token merges its V/BN partials -> lse, lp = x_y − lse.
 //
 // The GEMM is MFMA-bound (2·H FLOP per token·vocab pair); the partials cost 8 B per
 // (token, vocab tile) — 1/16 of writing the bf16 logits.
@@ -23,12 +23,27 @@ namespace trlx {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int kLmBM = 128;               // tokens per tile
-constexpr int kLmBN = 128;               // vocab entries per tile
-constexpr int kLmBK = 64;                // K per stage (one 128-B row of bf16 per tile row)
-constexpr int kLmThreads = 256;          // 4 waves, 2 (tokens) x 2 (vocab), 64 x 64 each
-constexpr int kLmStage = (kLmBM + kLmBN) * kLmBK * 2;  // 32 KB: A tile + B tile
-constexpr int kLmLds = 2 * kLmStage + kLmBM * 4;       // double buffer + the tile's labels
+constexpr int kLmBK = 64;  // K per stage: one 128-B row of bf16 per tile row
+
+// Workgroup tile BM tokens x BN vocab computed by WM x WN waves (each a (BM/WM) x (BN/WN)
+// block of 16x16 MFMA tiles).  Two instantiations: 256 x 256 by 8 waves (128 x 64 each: the
+// register blocking that keeps the LDS fragment traffic under the MFMA time) for large N,
+// 128 x 128 by 4 waves for small batches.
+template <int BM_, int BN_, int WM_, int WN_>
+struct LmGeom {
+    static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+    static constexpr int kWaves = WM * WN, kThreads = kWaves * kWave;
+    static constexpr int kWRows = BM / WM, kWCols = BN / WN;  // per-wave block
+    static constexpr int kMR = kWRows / 16, kNR = kWCols / 16;  // MFMA repeats
+    static constexpr int kStage = (BM + BN) * kLmBK * 2;        // A tile + B tile bytes
+    static constexpr int kGroupsA = BM / 8, kGroupsB = BN / 8;  // 1-KB glds groups (8 rows)
+    static constexpr int kGlds = (kGroupsA + kGroupsB) / kWaves;  // glds per lane per stage
+    static constexpr int kLds = 2 * kStage + BM * 4;            // double buffer + labels
+    static_assert(kGroupsA % kWaves == 0 && kGroupsB % kWaves == 0, "staging split");
+    static_assert(WN * BM * 8 <= 2 * kStage, "combine area");
+};
+typedef LmGeom<256, 256, 2, 4> LmBig;
+typedef LmGeom<128, 128, 2, 2> LmSmall;
 
 struct LmHeadArgs {
     const uint16_t* h;     // [N, H] rows of ldh elements
@@ -40,32 +55,37 @@ struct LmHeadArgs {
     float2* part;          // [N, nvt] (max, Σexp) per vocab tile
     float* xlab;           // [N] label logit
     int nvt;
+    int xcd_swizzle;       // 1: remap blockIdx so each XCD gets a contiguous range of tiles
 };
 
-// Swizzled LDS image of a [128 rows][64 k] bf16 tile: row r is 128 B; its 16-B chunk c sits
-// at physical chunk c ^ ((r >> 1) & 7).  A quarter-wave ds_read_b128 of one chunk column
-// over 16 consecutive rows then touches 16 distinct 4-bank groups (even / odd rows fall in
-// the two halves of the 256-B bank row): conflict-free.
+// Swizzled LDS image of a [rows][64 k] bf16 tile: row r is 128 B; its 16-B chunk c sits at
+// physical chunk c ^ ((r >> 1) & 7).  A quarter-wave ds_read_b128 of one chunk column over
+// 16 consecutive rows then touches 16 distinct 4-bank groups (even / odd rows fall in the
+// two halves of the 256-B bank row): conflict-free.  The map is an involution.
 __device__ __forceinline__ int lds_chunk(int r, int c) { return c ^ ((r >> 1) & 7); }
 
-// Stage k-step `kt` of the A (tokens) and B (vocab) tiles into `stage`: 16 wave-instructions
-// of 1 KB (8 rows) per operand, 4 + 4 per wave; each lane fetches the logical chunk that
-// lands at its lane-linear LDS slot.  Rows past N / V are clamped (their results are masked).
+// Stage k-step `kt` of the A (tokens) and B (vocab) tiles: 1-KB wave-instructions of 8 rows;
+// lane l lands at LDS slot l of its group (row l>>3, physical chunk l&7) and so fetches the
+// logical chunk of that slot.  Rows past N / V are clamped (their results are masked).
+template <class G>
 __device__ __forceinline__ void lm_stage(const LmHeadArgs& a, char* stage, int m0, int n0, int kt, int wave,
                                          int lane) {
     const int rl = lane >> 3, pc = lane & 7;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int g = wave * 4 + i;   // 8-row group
+    for (int i = 0; i < G::kGroupsA / G::kWaves; ++i) {
+        const int g = i * G::kWaves + wave;
         const int r = g * 8 + rl;
-        const int lc = lds_chunk(r, pc);  // the involution maps physical -> logical too
         const int ma = min(m0 + r, a.N - 1);
-        const uint16_t* srcA = a.h + int64_t(ma) * a.ldh + kt * kLmBK + lc * 8;
-        __builtin_amdgcn_global_load_lds(srcA, (__attribute__((address_space(3))) void*)(stage + g * 1024), 16, 0,
-                                         0);
+        const uint16_t* src = a.h + int64_t(ma) * a.ldh + kt * kLmBK + lds_chunk(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stage + g * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < G::kGroupsB / G::kWaves; ++i) {
+        const int g = i * G::kWaves + wave;
+        const int r = g * 8 + rl;
         const int nb = min(n0 + r, a.V - 1);
-        const uint16_t* srcB = a.w + int64_t(nb) * a.ldw + kt * kLmBK + lc * 8;
-        __builtin_amdgcn_global_load_lds(srcB, (__attribute__((address_space(3))) void*)(stage + kLmBM * 128 + g * 1024),
+        const uint16_t* src = a.w + int64_t(nb) * a.ldw + kt * kLmBK + lds_chunk(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stage + G::BM * 128 + g * 1024),
                                          16, 0, 0);
     }
 }
@@ -74,71 +94,82 @@ __device__ __forceinline__ bf16x8_t lds_frag(const char* tile, int r, int c) {
     return *reinterpret_cast<const bf16x8_t*>(tile + r * 128 + lds_chunk(r, c) * 16);
 }
 
-__global__ __launch_bounds__(kLmThreads) void k_lmhead_tiles(LmHeadArgs a) {
-    __shared__ __attribute__((aligned(16))) char smem[kLmLds];
+template <class G>
+__global__ __launch_bounds__(G::kThreads) void k_lmhead_tiles(LmHeadArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[G::kLds];  // ONE LDS object (glds waits)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
-    // token tiles fastest: consecutive workgroups share the vocab tile (its W rows stay in L2)
-    const int ntt = (a.N + kLmBM - 1) / kLmBM;
-    const int mt = blockIdx.x % ntt, vt = blockIdx.x / ntt;
-    const int m0 = mt * kLmBM, n0 = vt * kLmBN;
-    int* lab = reinterpret_cast<int*>(smem + 2 * kLmStage);
-    if (tid < kLmBM) {
-        const int m = m0 + tid;
-        lab[tid] = m < a.N ? int(a.labels[int64_t(m) * a.lb]) : -1;
+    const int wr = wave / G::WN, wc = wave % G::WN;
+    // token tiles fastest: consecutive tiles share the vocab tile (its W rows stay in L2).
+    // Workgroups are dealt round-robin to the 8 XCDs; with xcd_swizzle each XCD's share is a
+    // contiguous tile range (bijective remap, cdna_hip_programming.md T1) — speed only.
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    int b = blockIdx.x;
+    if (a.xcd_swizzle) {
+        const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = b % 8;
+        b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+    }
+    const int mt = b % ntt, vt = b / ntt;
+    const int m0 = mt * G::BM, n0 = vt * G::BN;
+    int* lab = reinterpret_cast<int*>(smem + 2 * G::kStage);
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        const int m = m0 + t;
+        lab[t] = m < a.N ? int(a.labels[int64_t(m) * a.lb]) : -1;
     }
 
-    f32x4_t acc[4][4];
+    f32x4_t acc[G::kMR][G::kNR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < G::kMR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     const int nk = a.H / kLmBK;
-    lm_stage(a, smem, m0, n0, 0, wave, lane);
+    lm_stage<G>(a, smem, m0, n0, 0, wave, lane);
     for (int kt = 0; kt < nk; ++kt) {
-        char* cur = smem + (kt & 1) * kLmStage;
+        const char* cur = smem + (kt & 1) * G::kStage;
         if (kt + 1 < nk) {
-            lm_stage(a, smem + ((kt + 1) & 1) * kLmStage, m0, n0, kt + 1, wave, lane);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt landed, kt+1 in flight
+            lm_stage<G>(a, smem + ((kt + 1) & 1) * G::kStage, m0, n0, kt + 1, wave, lane);
+            // tile kt landed (this wave's part), tile kt+1 stays in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::kGlds) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();  // ... and every other wave's part too
         const char* At = cur;
-        const char* Bt = cur + kLmBM * 128;
+        const char* Bt = cur + G::BM * 128;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < kLmBK / 32; ++ks) {
             const int c = ks * 4 + (lane >> 4);
-            bf16x8_t af[4], bfr[4];
+            bf16x8_t bfr[G::kNR];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) af[i] = lds_frag(At, wr * 64 + i * 16 + (lane & 15), c);
+            for (int j = 0; j < G::kNR; ++j) bfr[j] = lds_frag(Bt, wc * G::kWCols + j * 16 + (lane & 15), c);
+            __builtin_amdgcn_s_setprio(1);  // T5: favour this wave's MFMA issue over the partner's
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = lds_frag(Bt, wc * 64 + j * 16 + (lane & 15), c);
+            for (int i = 0; i < G::kMR; ++i) {
+                const bf16x8_t af = lds_frag(At, wr * G::kWRows + i * 16 + (lane & 15), c);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < G::kNR; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+            }
+            __builtin_amdgcn_s_setprio(0);
         }
         __builtin_amdgcn_s_barrier();  // every wave is done reading `cur` before it is restaged
     }
 
     // ---- epilogue: per token row, the tile's partial (max, Σexp) and the label logit
-    // acc[i][j][q] at lane l = logit(token m0 + wr*64 + i*16 + (l>>4)*4 + q,
-    //                                 vocab n0 + wc*64 + j*16 + (l&15))
-    float2* cmb = reinterpret_cast<float2*>(smem);  // [2 wc][128 rows], staging is free now
+    // acc[i][j][q] at lane l = logit(token m0 + wr*kWRows + i*16 + (l>>4)*4 + q,
+    //                                 vocab n0 + wc*kWCols + j*16 + (l&15))
+    float2* cmb = reinterpret_cast<float2*>(smem);  // [WN][BM], the staging buffers are free now
     const int cl = lane & 15;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < G::kMR; ++i) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int rt = wr * 64 + i * 16 + (lane >> 4) * 4 + q;  // row in tile
-            float x[4];
+            const int rt = wr * G::kWRows + i * 16 + (lane >> 4) * 4 + q;  // row in tile
+            float x[G::kNR];
             float mx = -INFINITY;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int v = n0 + wc * 64 + j * 16 + cl;
+            for (int j = 0; j < G::kNR; ++j) {
+                const int v = n0 + wc * G::kWCols + j * 16 + cl;
                 x[j] = v < a.V ? acc[i][j][q] : -INFINITY;
                 mx = fmaxf(mx, x[j]);
             }
@@ -148,26 +179,215 @@ __global__ __launch_bounds__(kLmThreads) void k_lmhead_tiles(LmHeadArgs a) {
             const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
             float s = 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s += exp2_fast(fmaf(x[j], kLog2e, ml2e));
+            for (int j = 0; j < G::kNR; ++j) s += exp2_fast(fmaf(x[j], kLog2e, ml2e));
 #pragma unroll
             for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, kWave);
-            if (cl == 0) cmb[wc * kLmBM + rt] = make_float2(mx, s);
-            const int dy = lab[rt] - (n0 + wc * 64);
-            if (dy >= 0 && dy < 64 && (dy & 15) == cl && m0 + rt < a.N) {
-                const int jy = dy >> 4;
-                a.xlab[m0 + rt] = jy == 0 ? x[0] : jy == 1 ? x[1] : jy == 2 ? x[2] : x[3];
+            if (cl == 0) cmb[wc * G::BM + rt] = make_float2(mx, s);
+            const int dy = lab[rt] - (n0 + wc * G::kWCols);
+            if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+                float xy = x[0];
+#pragma unroll
+                for (int j = 1; j < G::kNR; ++j) xy = (dy >> 4) == j ? x[j] : xy;
+                a.xlab[m0 + rt] = xy;
             }
         }
     }
     __syncthreads();
-    if (tid < kLmBM && m0 + tid < a.N) {
-        const float2 p0 = cmb[tid], p1 = cmb[kLmBM + tid];
-        const float m = fmaxf(p0.x, p1.x);
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        if (m0 + t >= a.N) continue;
+        float m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < G::WN; ++c) m = fmaxf(m, cmb[c * G::BM + t].x);
         float s = 0.f;
-        if (m != -INFINITY)
-            s = (p0.x == -INFINITY ? 0.f : p0.y * exp2_fast((p0.x - m) * kLog2e)) +
-                (p1.x == -INFINITY ? 0.f : p1.y * exp2_fast((p1.x - m) * kLog2e));
-        a.part[int64_t(m0 + tid) * a.nvt + vt] = make_float2(m, s);
+        if (m != -INFINITY) {
+#pragma unroll
+            for (int c = 0; c < G::WN; ++c) {
+                const float2 p = cmb[c * G::BM + t];
+                s += p.x == -INFINITY ? 0.f : p.y * exp2_fast((p.x - m) * kLog2e);
+            }
+        }
+        a.part[int64_t(m0 + t) * a.nvt + vt] = make_float2(m, s);
+    }
+}
+
+// ------------------------------------------------------------------ persistent, 3 stages in flight
+// One workgroup per CU walks its tiles (blockIdx.x, +gridDim.x, ...) as ONE stream of 32-deep
+// K-steps: four LDS stages, three in flight, and the stream runs straight across tile
+// boundaries — the next tile's first stages load while the current tile's epilogue runs, so
+// no tile pays the operand-fetch latency up front (at H = 768 a tile is only 24 K-steps).
+// One barrier per step: the wait for stage s, then the barrier that both publishes it and
+// frees stage s-1's buffer for the load of step s+3.  Every load of the loop is an LDS DMA
+// (an ordinary load would make hipcc drain the queue); the label logit is not picked out
+// here but recomputed by the combine kernel as one H-long dot product per token.
+constexpr int kPBK = 32;      // K per stage: 64-B rows
+constexpr int kPStages = 4;
+
+template <class G>
+struct LmPersist {
+    static constexpr int kStage = (G::BM + G::BN) * kPBK * 2;
+    static constexpr int kGroupsA = G::BM / 16, kGroupsB = G::BN / 16;  // 1-KB groups: 16 rows x 64 B
+    static constexpr int kGlds = (kGroupsA + kGroupsB) / G::kWaves;
+    static constexpr int kCmbOff = kPStages * kStage;
+    static constexpr int kLds = kCmbOff + G::WN * G::BM * 8;
+    static_assert(kGroupsA % G::kWaves == 0 && kGroupsB % G::kWaves == 0, "staging split");
+};
+
+// 64-B rows: chunk c of row r sits at c ^ ((r >> 2) & 3); the 16 rows a quarter-wave reads
+// then cover the 64 banks exactly once.
+__device__ __forceinline__ int lds_chunk64(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+__device__ __forceinline__ bf16x8_t lds_frag64(const char* tile, int r, int c) {
+    return *reinterpret_cast<const bf16x8_t*>(tile + r * 64 + lds_chunk64(r, c) * 16);
+}
+
+template <class G>
+__device__ __forceinline__ void lmp_stage(const LmHeadArgs& a, char* stage, int m0, int n0, int kt, int wave,
+                                          int lane) {
+    typedef LmPersist<G> P;
+    const int rl = lane >> 2, pc = lane & 3;
+#pragma unroll
+    for (int i = 0; i < P::kGroupsA / G::kWaves; ++i) {
+        const int g = i * G::kWaves + wave;
+        const int r = g * 16 + rl;
+        const int ma = min(m0 + r, a.N - 1);
+        const uint16_t* src = a.h + int64_t(ma) * a.ldh + kt * kPBK + lds_chunk64(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stage + g * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < P::kGroupsB / G::kWaves; ++i) {
+        const int g = i * G::kWaves + wave;
+        const int r = g * 16 + rl;
+        const int nb = min(n0 + r, a.V - 1);
+        const uint16_t* src = a.w + int64_t(nb) * a.ldw + kt * kPBK + lds_chunk64(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stage + G::BM * 64 + g * 1024),
+                                         16, 0, 0);
+    }
+}
+
+// An LDS store hipcc cannot see: a plain ds_write while LDS DMAs are in flight makes hipcc
+// wait vmcnt(0) first (it cannot prove the addresses differ), which would drain the three
+// stages in flight at every tile epilogue.  The combine area never overlaps a stage buffer.
+__device__ __forceinline__ void lds_store_f2(float2* p, float x, float y) {
+    const uint32_t addr = uint32_t(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float2*)p));
+    asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(make_float2(x, y)) : "memory");
+}
+
+__device__ __forceinline__ float2 lds_load_f2(const float2* p) {
+    const uint32_t addr = uint32_t(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const float2*)p));
+    float2 v;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+
+// s_waitcnt vmcnt(n) for the wave-uniform n of the pipeline (n in {0, g, 2g}).
+template <int GL>
+__device__ __forceinline__ void lmp_wait(int n) {
+    if (n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n == GL) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
+}
+
+template <class G>
+__global__ __launch_bounds__(G::kThreads) void k_lmhead_persist(LmHeadArgs a, int ntiles) {
+    typedef LmPersist<G> P;
+    __shared__ __attribute__((aligned(16))) char smem[P::kLds];  // ONE LDS object (glds waits)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / G::WN, wc = wave % G::WN;
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    const int nk = a.H / kPBK;
+    const int mine = (ntiles - int(blockIdx.x) + int(gridDim.x) - 1) / int(gridDim.x);
+    if (mine <= 0) return;
+    const int S = mine * nk;
+    float2* cmb = reinterpret_cast<float2*>(smem + P::kCmbOff);
+
+    auto loads_of = [&](int x) { return x >= S ? 0 : P::kGlds; };
+    auto issue = [&](int x) {
+        const int j = x / nk, kt = x - j * nk;
+        const int t = int(blockIdx.x) + j * int(gridDim.x);
+        const int mt = t % ntt, vt = t / ntt;
+        lmp_stage<G>(a, smem + (x % kPStages) * P::kStage, mt * G::BM, vt * G::BN, kt, wave, lane);
+    };
+
+    f32x4_t acc[G::kMR][G::kNR];
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int x = 0; x < 3 && x < S; ++x) issue(x);
+    for (int s = 0; s < S; ++s) {
+        lmp_wait<P::kGlds>(loads_of(s + 1) + loads_of(s + 2));  // stage s landed (this wave's part)
+        __builtin_amdgcn_s_barrier();  // ... every wave's part; and stage s-1's buffer is free
+        if (s + 3 < S) issue(s + 3);
+        const char* At = smem + (s % kPStages) * P::kStage;
+        const char* Bt = At + G::BM * 64;
+        const int c = lane >> 4;
+        bf16x8_t bfr[G::kNR];
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) bfr[j] = lds_frag64(Bt, wc * G::kWCols + j * 16 + (lane & 15), c);
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i) {
+            const bf16x8_t af = lds_frag64(At, wr * G::kWRows + i * 16 + (lane & 15), c);
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if (s % nk != nk - 1) continue;
+
+        // ---- tile epilogue (as k_lmhead_tiles), raw barriers: a __syncthreads() would drain
+        // the stages in flight
+        const int jt = s / nk;
+        const int t = int(blockIdx.x) + jt * int(gridDim.x);
+        const int m0 = (t % ntt) * G::BM, vt = t / ntt, n0 = vt * G::BN;
+        const int cl = lane & 15;
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rt = wr * G::kWRows + i * 16 + (lane >> 4) * 4 + q;
+                float xv[G::kNR];
+                float mx = -INFINITY;
+#pragma unroll
+                for (int j = 0; j < G::kNR; ++j) {
+                    const int v = n0 + wc * G::kWCols + j * 16 + cl;
+                    xv[j] = v < a.V ? acc[i][j][q] : -INFINITY;
+                    mx = fmaxf(mx, xv[j]);
+                }
+#pragma unroll
+                for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+                const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
+                float sm = 0.f;
+#pragma unroll
+                for (int j = 0; j < G::kNR; ++j) sm += exp2_fast(fmaf(xv[j], kLog2e, ml2e));
+#pragma unroll
+                for (int off = 1; off < 16; off <<= 1) sm += __shfl_xor(sm, off, kWave);
+                if (cl == 0) lds_store_f2(cmb + wc * G::BM + rt, mx, sm);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        for (int r = tid; r < G::BM; r += G::kThreads) {
+            if (m0 + r >= a.N) continue;
+            float2 pw[G::WN];
+            float m = -INFINITY;
+#pragma unroll
+            for (int c2 = 0; c2 < G::WN; ++c2) {
+                pw[c2] = lds_load_f2(cmb + c2 * G::BM + r);
+                m = fmaxf(m, pw[c2].x);
+            }
+            float sm = 0.f;
+            if (m != -INFINITY) {
+#pragma unroll
+                for (int c2 = 0; c2 < G::WN; ++c2)
+                    sm += pw[c2].x == -INFINITY ? 0.f : pw[c2].y * exp2_fast((pw[c2].x - m) * kLog2e);
+            }
+            a.part[int64_t(m0 + r) * a.nvt + vt] = make_float2(m, sm);
+        }
+        // the next tile's epilogue rewrites cmb only after many barriers
     }
 }
 
@@ -194,10 +414,26 @@ __global__ __launch_bounds__(256) void k_lmhead_combine(LmHeadArgs a, void* lp, 
                 (m2 == -INFINITY ? 0.f : s2 * exp2_fast((m2 - nm) * kLog2e));
         m = nm;
     }
+    // label logit: picked out by the tile kernel (xlab), or recomputed here as h[n]·W[y]
+    // (fp32 sum of the same exact bf16 products; one H-long dot per token)
+    const int64_t y = a.labels[n * a.lb];
+    const bool y_ok = y >= 0 && y < a.V;
+    float xy = 0.f;
+    if (a.xlab == nullptr && y_ok) {
+        const uint32_t* hr = reinterpret_cast<const uint32_t*>(a.h + n * a.ldh);
+        const uint32_t* wr = reinterpret_cast<const uint32_t*>(a.w + y * a.ldw);
+        for (int k = lane; k < a.H / 2; k += kWave) {
+            const uint32_t hv = hr[k], wv = wr[k];
+            xy = fmaf(bf_lo(hv), bf_lo(wv), xy);
+            xy = fmaf(bf_hi(hv), bf_hi(wv), xy);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) xy += __shfl_xor(xy, off, kWave);
+    }
     if (lane == 0) {
         const float lse = m + logf(s);
-        const int64_t y = a.labels[n * a.lb];
-        const float lpv = (y >= 0 && y < a.V) ? a.xlab[n] - lse : NAN;
+        if (a.xlab) xy = a.xlab[n];
+        const float lpv = y_ok ? xy - lse : NAN;
         st_any(lp, lp_dtype, n, lpv);
         if (lse_out) lse_out[n] = lse;
     }
@@ -207,9 +443,59 @@ __global__ __launch_bounds__(256) void k_lmhead_combine(LmHeadArgs a, void* lp, 
 
 using namespace trlx;
 
+// variant: 0 auto, 1 persistent 256x256 (BK 32, 3 stages in flight), 2 256x256 tiles, 3 128x128
+// tiles, 4 = 2 with the XCD remap
+// auto (measured on MI355X, tools/lmhead_bench.py): short K (H <= 1024, a tile is <= 32 K-steps)
+// -> persistent, which hides each tile's operand-fetch latency behind the previous tile;
+// long K -> the plain 256x256 tiles; small N -> 128x128 tiles (enough workgroups).
+static int g_lm_variant = 0;
+static int lm_variant(int64_t N, int64_t H = 0) {
+    if (g_lm_variant) return g_lm_variant;
+    if (N < 2048) return 3;
+    return H <= 1024 ? 1 : 2;
+}
+static int lm_tile_n(int64_t N) { return lm_variant(N) == 3 ? LmSmall::BN : LmBig::BN; }
+static_assert(LmSmall::BN == 128 && LmBig::BN == 256, "tile widths");
+
+extern "C" int trlx_lmhead_set_variant(int v) {
+    TRLX_REQUIRE(v >= 0 && v <= 4, TRLX_ERR_ARG, "lmhead variant 0..4");
+    g_lm_variant = v;
+    return TRLX_OK;
+}
+
+static int lm_num_cus() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
+template <class G>
+static int lm_launch_persist(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntiles = int64_t((a.N + G::BM - 1) / G::BM) * a.nvt;
+    TRLX_REQUIRE(ntiles < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    const int grid = int(ntiles < lm_num_cus() ? ntiles : lm_num_cus());
+    LmHeadArgs b = a;
+    b.xlab = nullptr;  // the combine kernel recomputes the label logit
+    hipLaunchKernelGGL((k_lmhead_persist<G>), dim3(grid), dim3(G::kThreads), 0, stream, b, int(ntiles));
+    return check_launch("k_lmhead_persist");
+}
+
 extern "C" int64_t trlx_lmhead_workspace_bytes(int64_t N, int64_t V) {
-    const int64_t nvt = (V + kLmBN - 1) / kLmBN;
+    const int64_t nvt = (V + lm_tile_n(N) - 1) / lm_tile_n(N);
     return N * nvt * int64_t(sizeof(float2)) + N * int64_t(sizeof(float));
+}
+
+template <class G>
+static int lm_launch(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntt = (a.N + G::BM - 1) / G::BM;
+    TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    hipLaunchKernelGGL((k_lmhead_tiles<G>), dim3(unsigned(ntt * a.nvt)), dim3(G::kThreads), 0, stream, a);
+    return check_launch("k_lmhead_tiles");
 }
 
 extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
@@ -236,15 +522,19 @@ extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void*
     a.V = int(V);
     a.labels = labels;
     a.lb = lb;
-    a.nvt = int((V + kLmBN - 1) / kLmBN);
+    const int bn = lm_tile_n(N);
+    a.nvt = int((V + bn - 1) / bn);
     a.part = static_cast<float2*>(workspace);
     a.xlab = reinterpret_cast<float*>(static_cast<char*>(workspace) + N * a.nvt * int64_t(sizeof(float2)));
-    const int64_t ntt = (N + kLmBM - 1) / kLmBM;
-    TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
-    hipLaunchKernelGGL(k_lmhead_tiles, dim3(unsigned(ntt * a.nvt)), dim3(kLmThreads), 0, (hipStream_t)stream, a);
-    int rc = check_launch("k_lmhead_tiles");
+    const int var = lm_variant(N, H);
+    a.xcd_swizzle = var == 4;
+    int rc = var == 1              ? lm_launch_persist<LmBig>(a, (hipStream_t)stream)
+             : var == 2 || var == 4 ? lm_launch<LmBig>(a, (hipStream_t)stream)
+                                    : lm_launch<LmSmall>(a, (hipStream_t)stream);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_lmhead_combine, dim3(unsigned((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a, lp_out,
+    LmHeadArgs c = a;
+    if (var == 1) c.xlab = nullptr;
+    hipLaunchKernelGGL(k_lmhead_combine, dim3(unsigned((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, c, lp_out,
                        lp_dtype, lse_out);
     return check_launch("k_lmhead_combine");
 }
