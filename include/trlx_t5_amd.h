@@ -296,6 +296,21 @@ int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, in
                          int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
                          int lp_dtype, float* lse_out, void* workspace, void* stream);
 
+/* ---------------------------------------------------------------- §8f rank 3: ILQL sampling step
+ * One decode step of CausalLMWithValueHeads.generate (ilql_models.py:296-316) per row b:
+ *   score = log_softmax(logits[b]) + beta*(min(tq0[b], tq1[b]) - vs[b])  (logits -inf where
+ *   logit_mask[prev_ids[b]] is set), topk_mask(score, top_k) (:24-28, ties at the threshold
+ *   kept), pi = softmax(. / temperature); out_ids[b] = the inverse CDF of pi at u[b] (index
+ *   order; u from the caller's generator replaces torch.multinomial's draw);
+ *   out = finished ? eos : out; finished = out == eos.
+ * logits / tq rows: [B, V] of dtype with row strides ld_*; tq1 may be NULL (one head);
+ * logit_mask: NULL or uint8 [*, V] rows of ld_mask; finished: int64 [B] in/out or NULL. */
+int trlx_ilql_sample(const void* logits, int64_t ld_logits, const void* tq0, int64_t ld_tq0,
+                     const void* tq1, int64_t ld_tq1, int dtype, const float* vs,
+                     const uint8_t* logit_mask, int64_t ld_mask, const int64_t* prev_ids, int64_t B,
+                     int64_t V, float beta, int top_k, float temperature, const float* u,
+                     int64_t* out_ids, int64_t* finished, int64_t eos, void* stream);
+
 /* ---------------------------------------------------------------- §8f: device-resident rollout store
  * Row copy between padded columnar [rows, W] buffers — replaces the reference's
  * `.cpu()` of the experience tensors, per-sample PPORLElement lists and the pad_sequence

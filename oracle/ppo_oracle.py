@@ -255,3 +255,12 @@ def ppo_collate(elems, pad_token_id):
         pad_sequence([e.values for e in elems], padding_value=0.0, batch_first=True),
         pad_sequence([e.rewards for e in elems], padding_value=0.0, batch_first=True),
     )
+
+
+# ------------------------------------------------------------------ ilql_models.py:24-28 (= utils/__init__.py:107-116)
+def topk_mask(xs, k):
+    """Scores outside each row's top k -> -inf; entries equal to the k-th value are kept."""
+    if k > xs.shape[-1]:
+        return xs
+    mintop = torch.topk(xs, k)[0][:, -1].unsqueeze(-1)
+    return torch.where(xs < mintop, -np.inf * torch.ones_like(xs, dtype=xs.dtype), xs)

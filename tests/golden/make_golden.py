@@ -460,6 +460,22 @@ def make_rollout_store(ppo_pipeline, ppo_types):
     np.savez_compressed(os.path.join(OUT, "rollout_store.npz"), **out)
 
 
+# --------------------------------------------------------------------------- §8f rank 3 sampling
+def make_topk(ilql_models):
+    """ilql_models.topk_mask (:24-28) on rows with ties at the threshold, -inf entries and
+    k > V (returned unchanged)."""
+    out = {}
+    g = gen(800)
+    xs = torch.randn(6, 37, generator=g)
+    xs[1, :5] = xs[1, 5]          # a 6-way tie
+    xs[2, ::3] = float("-inf")
+    xs[3] = torch.round(xs[3])    # many ties
+    out["xs"] = xs.numpy()
+    for k in (1, 5, 20, 37, 40):
+        out[f"k{k}"] = ilql_models.topk_mask(xs, k).numpy()
+    np.savez_compressed(os.path.join(OUT, "topk_mask.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(4)
     only = sys.argv[1:]
@@ -478,6 +494,8 @@ if __name__ == "__main__":
         make_ilql(ilql_models, ilql_types)
     if not only or "whiten" in only:
         make_whiten(modeling)
+    if not only or "topk" in only:
+        make_topk(ilql_models)
     if not only or "store" in only:
         make_rollout_store(*load_ppo_pipeline())
     for f in sorted(os.listdir(OUT)):

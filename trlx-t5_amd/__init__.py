@@ -8,8 +8,8 @@ Drop-in names (reference file:line in danyang-rainbow/trlx-t5):
       trlx/model/nn/ppo_models.py
   kl_penalty_rewards, prepare_scores
       trlx/orchestrator/ppo_orchestrator.py:96-112,163-167
-  ILQLConfig (.loss), ILQLBatch
-      trlx/model/nn/ilql_models.py:52-116, trlx/data/ilql_types.py
+  ILQLConfig (.loss), ILQLBatch, ilql_sample_step (one decode step of generate)
+      trlx/model/nn/ilql_models.py:52-116,296-316, trlx/data/ilql_types.py
   lm_head_logprobs — fused lm_head GEMM (MFMA) + logprobs, logits never in HBM
   PPORolloutStorage, PPORLElement, PPORLBatch
       trlx/pipeline/ppo_pipeline.py, trlx/data/ppo_types.py (device-resident store)
@@ -25,15 +25,15 @@ from .ppo import (STATS_KEYS, AdaptiveKLController, FixedKLController, PPOConfig
                   prepare_scores, stats_dict)
 from .lm_head import lm_head_logprobs
 from .rollout_store import PPORLBatch, PPORLElement, PPORolloutStorage
-from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig, ILQLHotPath
+from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig, ILQLHotPath, ilql_sample_step
 from .step import PPOHotPath
 
 __all__ = [
     "logprobs_from_logits", "whiten", "get_global_statistics", "RunningMoments", "flatten_dict", "moments",
     "grad_buffer_like", "PPOConfig", "AdaptiveKLController", "FixedKLController", "kl_penalty_rewards",
     "prepare_scores", "stats_dict", "STATS_KEYS", "PPOHotPath", "load_library",
-    "ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS", "PPORolloutStorage", "PPORLElement", "PPORLBatch",
-    "lm_head_logprobs",
+    "ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS", "ilql_sample_step", "PPORolloutStorage",
+    "PPORLElement", "PPORLBatch", "lm_head_logprobs",
 ]
 
 

@@ -4,6 +4,8 @@
   ILQLConfig.loss   ilql_models.py:52-116 (CQL / AWAC cross-entropies over V, TD and
                                            expectile V losses, with autograd)
   ILQLBatch         trlx/data/ilql_types.py:30-49
+  ilql_sample_step  ilql_models.py:296-316 (one decode step of generate: log_softmax +
+                    beta*adv, topk_mask, softmax / temperature, the draw) — §8f rank 3
 
 The loss runs as three launches (include/trlx_t5_amd.h, trlx_ilql_*): every logits row and
 every Q-head row is read once and its gradient row written once in the forward; the
@@ -19,7 +21,7 @@ from . import _lib
 from .modeling import grad_buffer_like
 from .timing import make_event
 
-__all__ = ["ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS"]
+__all__ = ["ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS", "ilql_sample_step"]
 
 # stats keys in the reference's order (its dict comprehension walks locals(): loss_q,
 # loss_v, loss_cql, loss_awac, loss — ilql_models.py:109-113)
@@ -245,3 +247,47 @@ class ILQLHotPath:
         self._timed("rows", s, lambda: _lib.call("trlx_ilql_rows", ref, s.cuda_stream))
         self._timed("finalize", s, lambda: _lib.call("trlx_ilql_finalize", ref, s.cuda_stream))
         return self.losses, self.dlogits, self.dq, self.dvs
+
+
+def ilql_sample_step(logits, target_qs, vs, beta=1.0, top_k=20, temperature=1.0, logit_mask=None,
+                     input_ids=None, finished=None, eos_token_id=50256, generator=None):
+    """One token of CausalLMWithValueHeads.generate (ilql_models.py:296-316) on MI355X.
+
+    logits [B, V] (the last position), target_qs: one or two [B, V] heads, vs [B] or [B, 1];
+    logit_mask: optional bool [V', V] indexed by input_ids[:, -1]; finished: optional int64
+    [B] or [B, 1], updated in place.  Returns the sampled ids [B, 1] (int64).  The draw is
+    the inverse CDF of pi at uniforms from `generator` (torch.rand on the device) instead of
+    torch.multinomial's internal draw: same distribution, different random stream."""
+    target_qs = list(target_qs) if isinstance(target_qs, (list, tuple)) else [target_qs]
+    if len(target_qs) not in (1, 2):
+        raise ValueError("one or two target Q heads")
+    _lib.require_cuda(logits, vs, *target_qs)
+    if logits.dim() != 2:
+        raise ValueError("logits must be [B, V] (the last position)")
+    B, V = logits.shape
+    for q in target_qs:
+        if tuple(q.shape) != (B, V) or q.dtype != logits.dtype:
+            raise ValueError("target Q heads must match logits in shape and dtype")
+    rows = [t if t.stride(-1) == 1 else t.contiguous() for t in [logits] + target_qs]
+    v = vs.reshape(B).to(torch.float32).contiguous()
+    dev = logits.device
+    u = torch.rand(B, generator=generator, device=dev, dtype=torch.float32)
+    out = torch.empty(B, dtype=torch.int64, device=dev)
+    fin = None
+    if finished is not None:
+        fin = finished.reshape(B)
+        if fin.dtype != torch.int64 or not fin.is_contiguous() or fin.data_ptr() != finished.data_ptr():
+            raise ValueError("finished must be a contiguous int64 tensor (updated in place)")
+    mask = prev = None
+    if logit_mask is not None:
+        if input_ids is None:
+            raise ValueError("logit_mask needs input_ids")
+        mask = logit_mask.to(device=dev, dtype=torch.uint8).contiguous()
+        prev = input_ids[:, -1].to(device=dev, dtype=torch.int64).contiguous()
+    q1 = rows[2] if len(rows) > 2 else None
+    _lib.call("trlx_ilql_sample", rows[0].data_ptr(), rows[0].stride(0), rows[1].data_ptr(), rows[1].stride(0),
+              _lib.ptr(q1), 0 if q1 is None else q1.stride(0), _lib.dtype_code(rows[0]), v.data_ptr(),
+              _lib.ptr(mask), 0 if mask is None else mask.stride(0), _lib.ptr(prev), B, V, float(beta), int(top_k),
+              float(temperature), u.data_ptr(), out.data_ptr(), _lib.ptr(fin), int(eos_token_id),
+              _lib.stream_of(logits))
+    return out.view(B, 1)
