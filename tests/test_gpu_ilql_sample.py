@@ -78,6 +78,35 @@ def test_sample_inverse_cdf_vs_oracle(V, top_k, nq, dtype):
     check_draws(tok, pi, score, u, top_k)
 
 
+@pytest.mark.parametrize("V,top_k,quant,dtype", [
+    (3000, 20, 0.0, torch.float32),     # every score tied: more candidates than the LDS list -> bisection
+    (1000, 5, 0.0, torch.float32),      # every score tied, list fits, 1000 kept > one-wave draw cap
+    (50257, 600, None, torch.float32),  # k above the 512 threads of the long-row kernel
+    (50257, 1000, None, torch.bfloat16),
+    (20000, 50, 0.5, torch.float32),    # coarse values: heavy ties at the threshold
+    (50257, 20, 1.0, torch.bfloat16)])
+def test_sample_fallback_paths(V, top_k, quant, dtype):
+    """Rows that defeat the candidate pre-filter (ties, large k) take the block-wide paths;
+    every path must give the inverse-CDF token of the oracle's pi."""
+    B = 8
+    g = torch.Generator().manual_seed(V + top_k)
+    if quant == 0.0:
+        logits = torch.zeros(B, V)
+        tqs = [torch.zeros(B, V) for _ in range(2)]
+    else:
+        logits = torch.randn(B, V, generator=g) * 3
+        tqs = [torch.randn(B, V, generator=g) for _ in range(2)]
+        if quant:
+            logits, tqs = (logits / quant).round() * quant, [(t / quant).round() * quant for t in tqs]
+    logits, tqs = logits.to(dtype), [t.to(dtype) for t in tqs]
+    vs = torch.randn(B, generator=g)
+    u = torch.rand(B, generator=g)
+    u[0], u[1] = 0.0, 0.999999
+    tok, _ = sample_abi(logits, tqs, vs, 2.0, top_k, 0.7, u)
+    pi, score = oracle_pi(logits.float(), [t.float() for t in tqs], vs, 2.0, top_k, 0.7)
+    check_draws(tok, pi, score, u, top_k)
+
+
 def test_sample_distribution_matches_pi():
     """Many draws of one row: empirical frequencies vs pi (the multinomial it replaces)."""
     V, top_k, n = 40, 8, 20000

@@ -38,15 +38,15 @@ def torch_step(logits, tqs, vs, beta, k, temp):
 
 def main():
     dev = torch.device("cuda:0")
-    for B in (8, 32, 128):
+    for dt, B in [(torch.float32, b) for b in (8, 32, 128)] + [(torch.bfloat16, b) for b in (8, 128)]:
         V = 50257
         g = torch.Generator(device=dev).manual_seed(0)
-        logits = torch.randn(B, V, generator=g, device=dev)
-        tqs = [torch.randn(B, V, generator=g, device=dev) for _ in range(2)]
-        vs = torch.randn(B, 1, generator=g, device=dev)
+        logits = torch.randn(B, V, generator=g, device=dev).to(dt)
+        tqs = [torch.randn(B, V, generator=g, device=dev).to(dt) for _ in range(2)]
+        vs = torch.randn(B, 1, generator=g, device=dev).to(dt)
         ours = timeit(lambda: P.ilql_sample_step(logits, tqs, vs, beta=4.0, top_k=20, generator=g))
         ref = timeit(lambda: torch_step(logits, tqs, vs, 4.0, 20, 1.0))
-        print(f"B={B:4d} V={V}: fused sampling step {ours:8.1f} us | torch ops (reference step) {ref:8.1f} us"
+        print(f"{str(dt)[6:]:8s} B={B:4d} V={V}: fused sampling step {ours:8.1f} us | torch ops (reference step) {ref:8.1f} us"
               f" | {ref / ours:5.2f}x")
 
 
