@@ -6,7 +6,9 @@
 One "step" = one PPOHotPath.step over one shard of synthetic rollouts (see
 trlx-t5_amd/step.py): policy+reference log-softmax-gather (experience), fused KL reward
 + GAE + whitening moments (+ RCCL all-reduce when N > 1), fused new-policy logprob + PPO
-gradient + dlogits write, value loss + stats.  Inputs are resident in HBM before timing.
+gradient + dlogits write, value loss + stats; the score RunningMoments / clip and the
+adaptive KL controller run on device inside the two rollout tails (PPOControlState,
+configs/ppo_config.yml settings; --host-state for a host-constant beta).  Inputs are resident in HBM before timing.
 Weak scaling: every rank processes its own shard of the configuration's per-GPU batch;
 `value` = all ranks' tokens / max-over-ranks wall time.
 
@@ -49,6 +51,9 @@ def parse():
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--no-timers", action="store_true", help="skip per-kernel HIP events")
+    p.add_argument("--host-state", action="store_true",
+                   help="PPO: keep beta as a host constant and skip the score RunningMoments/clip and the KL "
+                        "controller update (the default runs them on device, ppo_config.yml settings)")
     p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -169,16 +174,21 @@ def cpu_baseline(torch, T, V, seconds):
     old_values = torch.randn(Bs, T, generator=g).to(bf)
     values = (old_values.float() + 0.3 * torch.randn(Bs, T, generator=g)).to(bf)
     scores = torch.rand(Bs, generator=g) * 24 - 12
+    sc = orc.ScoreControl(False, 10)
+    kl = orc.AdaptiveKLController(0.05, 6, 10000)
     toks, t0 = 0, time.perf_counter()
     while True:
-        orc.ppo_step_reference(logits, ref_logits, new_logits, labels, old_values, values, scores, kl_coef=0.05)
+        s_t, _, _ = sc(scores)
+        r = orc.ppo_step_reference(logits, ref_logits, new_logits, labels, old_values, values, s_t,
+                                   kl_coef=kl.value)
+        kl.update(float(r["stats"]["policy/approx_kl"]), n_steps=Bs)
         toks += Bs * T
         el = time.perf_counter() - t0
         if el >= seconds:
             break
     return {"value": toks / el, "unit": "tokens/s", "cores": cores, "kind": "port",
-            "sample": f"{toks // (Bs * T)} steps of {Bs}x{T}x{V} bf16 (oracle.ppo_step_reference: reference ops "
-                      f"incl. autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
+            "sample": f"{toks // (Bs * T)} steps of {Bs}x{T}x{V} bf16 (oracle ScoreControl + ppo_step_reference + "
+                      f"AdaptiveKLController: reference ops incl. autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
 
 
 def main():
@@ -213,7 +223,9 @@ def main():
             return hp.step(lg, qs, tqs, vs, batch)
     else:
         x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked)
-        hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05)
+        cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
+        ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
+        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl)
 
         def step():
             return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],

@@ -325,6 +325,78 @@ int trlx_rows_copy(int nfields, const void* const* src, void* const* dst, const 
                    const int64_t* cols, const int* esize, int64_t rows, const int64_t* src_idx,
                    int64_t src_row0, const int64_t* dst_idx, int64_t dst_row0, void* stream);
 
+/* ---------------------------------------------------------------- §8f rank 4: device-resident controller state
+ * The PPO loop's host scalars — RunningMoments of the scores (trlx/utils/modeling.py:72-104),
+ * the orchestrator's ref_mean/ref_std + score scale/clip (ppo_orchestrator.py:48-49,96-112)
+ * and the KL coefficient of Adaptive/FixedKLController (ppo_models.py:26-58) — as ONE fp64
+ * record in device memory, read and advanced in-stream (no host synchronisation).
+ * Slots (doubles): */
+#define TRLX_CTL_SLOTS 16
+#define TRLX_CTL_MEAN 0          /* RunningMoments.mean  */
+#define TRLX_CTL_VAR 1           /* RunningMoments.var   */
+#define TRLX_CTL_STD 2           /* RunningMoments.std   */
+#define TRLX_CTL_COUNT 3         /* RunningMoments.count */
+#define TRLX_CTL_REF_MEAN 4      /* orchestrator ref_mean */
+#define TRLX_CTL_REF_STD 5       /* orchestrator ref_std  */
+#define TRLX_CTL_REF_SET 6       /* 1 once ref_mean is known (config or first batch) */
+#define TRLX_CTL_KL_COEF 7       /* kl_ctl.value (beta) */
+#define TRLX_CTL_BATCH_MEAN 8    /* last RunningMoments.update return values */
+#define TRLX_CTL_BATCH_STD 9
+#define TRLX_CTL_KL_UPDATES 10   /* number of kl_ctl.update calls */
+#define TRLX_CTL_LAST_KL 11      /* last approx_kl given to kl_ctl.update */
+
+typedef enum {
+    TRLX_SCALE_NONE = 0,     /* scale_reward False */
+    TRLX_SCALE_RUNNING = 1,  /* "running": scores /= running.std */
+    TRLX_SCALE_REF = 2,      /* "ref": scores /= ref_std */
+} trlx_scale_mode;
+
+/* Score-side control: RunningMoments.update(scores) (global moments when given: the
+ * all-reduced {Σx, Σx², n} of trlx_score_moments over ranks, else the local batch), the
+ * first-batch ref_mean/ref_std, then scores = clip(scores / scale, ±cliprange_reward). */
+typedef struct {
+    const double* state_in;          /* [TRLX_CTL_SLOTS] */
+    double* state_out;               /* [TRLX_CTL_SLOTS], may equal state_in only in trlx_score_ctl_update */
+    const double* global_moments;    /* [>=3] or NULL */
+    int scale_mode;                  /* trlx_scale_mode */
+    float cliprange_reward;          /* 0 = no clip */
+} trlx_score_ctl;
+
+/* KL-side control: kl_ctl.update(approx_kl, n_steps) on state (in place). */
+typedef struct {
+    double* state;                   /* [TRLX_CTL_SLOTS] */
+    int adaptive;                    /* 1 AdaptiveKLController, 0 FixedKLController */
+    double target, horizon;
+    int64_t n_steps;                 /* config.train.batch_size (accelerate_ppo_model.py:131) */
+} trlx_kl_ctl;
+
+/* state = {mean 0, var 1, std 1, count 1e-24, ref_mean, ref_std, ref_set, init_kl_coef, ...}
+ * (RunningMoments.__init__, modeling.py:78-81; orchestrator :48-49; kl_ctl init). */
+int trlx_ctl_init(double* state, double init_kl_coef, double ref_mean, double ref_std, int ref_set,
+                  void* stream);
+/* {Σx, Σx², n, 0} of scores (fp64, one workgroup) — the record a caller all-reduces across
+ * ranks before trlx_score_ctl_update / trlx_ppo_rollout_gae_ctl. */
+int trlx_score_moments(const void* scores, int dtype, int64_t n, double* moments, void* stream);
+/* One workgroup: the score-side control above; scores_out (may alias scores) receives the
+ * scaled, clipped scores.  ppo_orchestrator.py:96-112. */
+int trlx_score_ctl_update(const void* scores, int dtype, int64_t n, const trlx_score_ctl* ctl,
+                          void* scores_out, int out_dtype, void* stream);
+/* kl_ctl.update with approx_kl read from device memory (fp32, e.g. the loss stats slot 8). */
+int trlx_kl_ctl_update(const trlx_kl_ctl* kl, const float* approx_kl, void* stream);
+/* The fused step's tails with the controller state folded in (no extra launch):
+ *   trlx_ppo_rollout_gae_ctl  = trlx_ppo_rollout_gae with beta read from ctl->state_in and
+ *                               the scores passed through the score-side control (every
+ *                               block derives the same values; block 0 writes state_out,
+ *                               which must not alias state_in);
+ *   trlx_ppo_rollout_loss_ctl = trlx_ppo_rollout_loss + kl_ctl.update(approx_kl) by the
+ *                               block that writes the stats. */
+int trlx_ppo_rollout_gae_ctl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                             int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                             const trlx_score_ctl* ctl, float gamma, float lam, float* rewards, float* adv_raw,
+                             void* ret, int ret_dtype, double* stats, void* workspace, void* stream);
+int trlx_ppo_rollout_loss_ctl(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                              float* loss_stats, void* workspace, const trlx_kl_ctl* kl, void* stream);
+
 /* ---------------------------------------------------------------- autograd plumbing
  * out[i] = x[i] * (*scale) for i < n (scale: device fp32 scalar, e.g. a backward's
  * grad_output).  In place (out == x) it is skipped entirely when *scale == 1. */

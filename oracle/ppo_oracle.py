@@ -160,6 +160,29 @@ def prepare_scores(scores, running, scale_reward, cliprange_reward, ref_std=None
     return scores, m, s
 
 
+class ScoreControl:
+    """The orchestrator's score bookkeeping, ppo_orchestrator.py:48-49 (init from the method
+    config) and :96-112 (first-batch ref stats, RunningMoments.update, scale, clip)."""
+
+    def __init__(self, scale_reward=False, cliprange_reward=10, ref_mean=None, ref_std=None):
+        self.running = RunningMoments()
+        self.ref_mean, self.ref_std = ref_mean, ref_std
+        self.scale_reward, self.cliprange_reward = scale_reward, cliprange_reward
+
+    def __call__(self, scores):
+        scores = scores.clone()
+        if self.ref_mean is None:
+            self.ref_mean, self.ref_std = scores.mean(), scores.std()
+        batch_mean, batch_std = self.running.update(scores)
+        if self.scale_reward == "running":
+            scores /= self.running.std
+        elif self.scale_reward == "ref":
+            scores /= self.ref_std
+        if self.cliprange_reward:
+            scores = torch.clip(scores, -self.cliprange_reward, self.cliprange_reward)
+        return scores, batch_mean, batch_std
+
+
 def kl_penalty_rewards(logprobs, ref_logprobs, kl_coef, scores=None, lengths=None):
     """ppo_orchestrator.py:164-167.  With `lengths` (build extension for the padded store,
     ppo_pipeline.py:47-65): the score goes to column lengths[b]-1 and later columns are 0."""

@@ -50,3 +50,28 @@ def hot_path_step_worker(rank, world, port, inputs, q):
                   "stats": stats.cpu()}))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def ctl_step_worker(rank, world, port, inputs, scores_seq, scale, q):
+    """Two DP steps with the device controller state: the score moments are all-reduced
+    (get_global_statistics semantics for RunningMoments), ref stats stay rank-local
+    (scores.std() of the rank's chunk, ppo_orchestrator.py:96-98)."""
+    import torch.distributed as dist
+    import trlx_t5_amd as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    sh = {k: (v.chunk(world, dim=0)[rank].contiguous().to(dev) if v is not None else None) for k, v in inputs.items()}
+    B, T, V = sh["logits"].shape
+    cfg = P.PPOConfig(scale_reward=scale, cliprange_reward=10)
+    ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B)
+    hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.0, ctl=ctl)
+    out = []
+    for s in scores_seq:
+        hp.step(sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"], sh["old_values"], sh["values"],
+                s.chunk(world)[rank].contiguous().to(dev))
+        torch.cuda.synchronize()
+        out.append({"rewards": hp.rewards.cpu(), "state": ctl.host(), "approx_kl": float(hp.stats[8])})
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()

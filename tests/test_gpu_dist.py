@@ -75,3 +75,53 @@ def test_dp2_step_global_whitening(lengths):
         torch.testing.assert_close(got["loss"].reshape(()), loss.detach(), rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(got["dlogits"], xg.grad, rtol=2e-2, atol=1e-6)
         torch.testing.assert_close(got["dvalues"], vg.grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("scale", ["running", "ref"])
+def test_dp2_device_state(scale):
+    """Device RunningMoments across ranks: every rank merges the GLOBAL score moments (one
+    all-reduce of {Σx, Σx², n}), so all ranks hold the same running statistics; ref_std is
+    each rank's own first-chunk std; beta advances rank-locally from the rank's approx_kl
+    (accelerate_ppo_model.py:123,130-131)."""
+    import torch.multiprocessing as mp
+    import dist_workers
+    world, B, T, V = 2, 8, 12, 517
+    x = _inputs(B, T, V, 21, False)
+    g = torch.Generator().manual_seed(9)
+    seq = [torch.randn(B, generator=g) * 12 + 1, torch.randn(B, generator=g) * 3 - 2]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + os.getpid() % 150
+    ps = [ctx.Process(target=dist_workers.ctl_step_worker, args=(r, world, port, x, seq, scale, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    f = {k: (v.float() if v is not None and v.is_floating_point() else v) for k, v in x.items()}
+    lp = orc.logprobs_from_logits(f["logits"], x["labels"])
+    ref_lp = orc.logprobs_from_logits(f["ref_logits"], x["labels"])
+    running = orc.RunningMoments()  # single-process over the concatenated batch == the global statistics
+    ref_std = [None] * world
+    betas = [0.05] * world
+    for i, s in enumerate(seq):
+        running.update(s.clone())
+        for r in range(world):
+            rows = slice(r * B // world, (r + 1) * B // world)
+            sr = s[rows].clone()
+            if ref_std[r] is None:
+                ref_std[r] = sr.std()
+            sr = sr / (running.std if scale == "running" else ref_std[r])
+            sr = torch.clip(sr, -10, 10)
+            want = orc.kl_penalty_rewards(lp[rows], ref_lp[rows], betas[r], sr)
+            got = res[r][i]
+            torch.testing.assert_close(got["rewards"], want, rtol=1e-5, atol=1e-5)
+            assert got["state"]["std"] == pytest.approx(float(running.std), rel=1e-5)
+            assert got["state"]["count"] == pytest.approx(float(running.count), rel=1e-12)
+            assert got["state"]["ref_std"] == pytest.approx(float(ref_std[r]), rel=1e-5)
+            kl = orc.AdaptiveKLController(betas[r], 6, 10000)
+            kl.update(got["approx_kl"], n_steps=B // world)
+            betas[r] = kl.value
+            assert got["state"]["kl_coef"] == betas[r]

@@ -14,6 +14,7 @@ Drop-in names (reference file:line in danyang-rainbow/trlx-t5):
   PPORolloutStorage, PPORLElement, PPORLBatch
       trlx/pipeline/ppo_pipeline.py, trlx/data/ppo_types.py (device-resident store)
   PPOHotPath — the fused device-resident experience+loss step (bench / DP shard)
+  PPOControlState — RunningMoments / score scale+clip / KL controller state in HBM
 
 All tensor math runs in hand-written HIP kernels (libtrlx_t5_amd.so, C ABI in
 include/trlx_t5_amd.h).  There is no CPU fallback.
@@ -26,6 +27,7 @@ from .ppo import (STATS_KEYS, AdaptiveKLController, FixedKLController, PPOConfig
 from .lm_head import lm_head_logprobs
 from .rollout_store import PPORLBatch, PPORLElement, PPORolloutStorage
 from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig, ILQLHotPath, ilql_sample_step
+from .control import PPOControlState
 from .step import PPOHotPath
 
 __all__ = [
@@ -33,7 +35,7 @@ __all__ = [
     "grad_buffer_like", "PPOConfig", "AdaptiveKLController", "FixedKLController", "kl_penalty_rewards",
     "prepare_scores", "stats_dict", "STATS_KEYS", "PPOHotPath", "load_library",
     "ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS", "ilql_sample_step", "PPORolloutStorage",
-    "PPORLElement", "PPORLBatch", "lm_head_logprobs",
+    "PPORLElement", "PPORLBatch", "lm_head_logprobs", "PPOControlState",
 ]
 
 

@@ -43,6 +43,26 @@ class IlqlArgs(ctypes.Structure):
 
 _ilql_p = ctypes.POINTER(IlqlArgs)
 
+CTL_SLOTS = 16
+(CTL_MEAN, CTL_VAR, CTL_STD, CTL_COUNT, CTL_REF_MEAN, CTL_REF_STD, CTL_REF_SET, CTL_KL_COEF, CTL_BATCH_MEAN,
+ CTL_BATCH_STD, CTL_KL_UPDATES, CTL_LAST_KL) = range(12)
+SCALE_NONE, SCALE_RUNNING, SCALE_REF = 0, 1, 2
+
+
+class ScoreCtl(ctypes.Structure):
+    """Mirror of trlx_score_ctl (include/trlx_t5_amd.h)."""
+    _fields_ = [("state_in", _c_vp), ("state_out", _c_vp), ("global_moments", _c_vp), ("scale_mode", _c_int),
+                ("cliprange_reward", _c_f)]
+
+
+class KlCtl(ctypes.Structure):
+    """Mirror of trlx_kl_ctl (include/trlx_t5_amd.h)."""
+    _fields_ = [("state", _c_vp), ("adaptive", _c_int), ("target", _c_d), ("horizon", _c_d), ("n_steps", _c_i64)]
+
+
+_score_ctl_p = ctypes.POINTER(ScoreCtl)
+_kl_ctl_p = ctypes.POINTER(KlCtl)
+
 # name -> (restype, argtypes)   (must match include/trlx_t5_amd.h exactly)
 SIGNATURES = {
     "trlx_abi_version": (_c_int, []),
@@ -96,6 +116,14 @@ SIGNATURES = {
                                   _c_i64, _c_i64, _c_f, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_rows_copy": (_c_int, [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp,
                                 _c_i64, _c_vp, _c_i64, _c_vp]),
+    "trlx_ctl_init": (_c_int, [_c_vp, _c_d, _c_d, _c_d, _c_int, _c_vp]),
+    "trlx_score_moments": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
+    "trlx_score_ctl_update": (_c_int, [_c_vp, _c_int, _c_i64, _score_ctl_p, _c_vp, _c_int, _c_vp]),
+    "trlx_kl_ctl_update": (_c_int, [_kl_ctl_p, _c_vp, _c_vp]),
+    "trlx_ppo_rollout_gae_ctl": (_c_int, [_c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
+                                          _score_ctl_p, _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                          _c_vp]),
+    "trlx_ppo_rollout_loss_ctl": (_c_int, [_c_i64, _c_i64, _c_vp, _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
     "trlx_ilql_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_int]),
     "trlx_ilql_prep": (_c_int, [_ilql_p, _c_vp]),
     "trlx_ilql_rows": (_c_int, [_ilql_p, _c_vp]),

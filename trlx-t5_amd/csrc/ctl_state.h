@@ -1,0 +1,125 @@
+// Device-resident controller state of the PPO loop: the reward
+// RunningMoments (trlx/utils/modeling.py:72-104), the score scale / clip of the
+// orchestrator (trlx/orchestrator/ppo_orchestrator.py:96-112) and the KL coefficient of
+// AdaptiveKLController / FixedKLController (trlx/model/nn/ppo_models.py:26-58) live in one
+// fp64 record in HBM (TRLX_CTL_SLOTS doubles, layout in trlx_t5_amd.h), so a PPO step reads
+// and advances them in-stream with no host synchronisation.
+//
+// The reference keeps these as Python scalars / 0-d tensors and reads them back every
+// chunk (`.item()`-style host round trips in the KL controller, RunningMoments attributes
+// as Python numbers).  Here the scalar arithmetic runs in fp64 on thread 0 of whichever
+// block needs it; the batch moments are block reductions over the (small) score vector.
+#pragma once
+#include "common.h"
+
+namespace trlx {
+
+struct ScoreCtlArgs {
+    const double* state_in;    // [TRLX_CTL_SLOTS]
+    double* state_out;         // [TRLX_CTL_SLOTS] (written by one block only)
+    const double* global_mom;  // {Σx, Σx², n} over all ranks, or NULL (local = global)
+    int scale_mode;            // TRLX_SCALE_*
+    float clip;                // cliprange_reward (0: no clip)
+};
+
+struct KlCtlArgs {
+    double* state;  // NULL: no KL update
+    int adaptive;
+    double target, horizon, n_steps;
+};
+
+// Divide-and-clip of one score (ppo_orchestrator.py:104-112): fp32 division by the fp32
+// scale (the reference divides fp32 tensors), then torch.clip.  div == 0 => no scaling.
+__device__ __forceinline__ float score_transform(float x, float div, float clip) {
+    if (div != 0.0f) x = __fdiv_rn(x, div);
+    if (clip != 0.0f) x = fminf(fmaxf(x, -clip), clip);
+    return x;
+}
+
+// RunningMoments.update + the reference-statistics bookkeeping + the scale choice, for
+// the whole block (every thread must call it; it contains barriers).  Batch moments of
+// scores[0, n): two fp64 passes (mean, then Σ(x - mean)²) -> the local statistics; the
+// running merge uses global_mom when given (get_global_statistics across ranks,
+// modeling.py:9-21, biased variance) and the local ones otherwise (torch.var_mean,
+// unbiased=False, modeling.py:86-87).  First call with ref unset: ref_mean / ref_std =
+// scores.mean(), scores.std() of the LOCAL batch (ppo_orchestrator.py:96-98, unbiased).
+// Outputs (all threads): the fp32 divisor for score_transform (0 = none) and beta.
+// When `writer`, thread 0 stores the advanced record to state_out.
+__device__ __forceinline__ void score_ctl_block(const ScoreCtlArgs& c, const float* scores, int n, bool writer,
+                                                float& div, float& beta) {
+    __shared__ double s_red[2 * (1024 / kWave)];
+    __shared__ float s_out[2];
+    const int nw = blockDim.x / kWave;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += double(scores[i]);
+    s = block_sum_d(s, s_red);
+    const double lmean = s / double(n);
+    double m2 = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const double d = double(scores[i]) - lmean;
+        m2 = fma(d, d, m2);
+    }
+    m2 = block_sum_d(m2, s_red + nw);
+    if (threadIdx.x == 0) {
+        double st[TRLX_CTL_SLOTS];
+#pragma unroll
+        for (int k = 0; k < TRLX_CTL_SLOTS; ++k) st[k] = c.state_in[k];
+        double xn, xm, xv;
+        if (c.global_mom) {
+            xn = c.global_mom[2];
+            xm = c.global_mom[0] / xn;
+            xv = fmax(c.global_mom[1] - c.global_mom[0] * xm, 0.0) / xn;
+        } else {
+            xn = double(n);
+            xm = lmean;
+            xv = m2 / xn;
+        }
+        // Chan merge, term for term as modeling.py:91-102
+        const double delta = xm - st[TRLX_CTL_MEAN];
+        const double cnt = st[TRLX_CTL_COUNT];
+        const double tot = cnt + xn;
+        const double new_sum = xv * xn;
+        const double old_sum = st[TRLX_CTL_VAR] * cnt + delta * delta * cnt * xn / tot;
+        st[TRLX_CTL_MEAN] += delta * xn / tot;
+        st[TRLX_CTL_VAR] = (old_sum + new_sum) / tot;
+        st[TRLX_CTL_STD] = sqrt(st[TRLX_CTL_VAR] * tot / (tot - 1.0));
+        st[TRLX_CTL_COUNT] = tot;
+        st[TRLX_CTL_BATCH_MEAN] = xm;
+        st[TRLX_CTL_BATCH_STD] = sqrt(xv * xn / (xn - 1.0));
+        if (st[TRLX_CTL_REF_SET] == 0.0) {
+            st[TRLX_CTL_REF_MEAN] = lmean;
+            st[TRLX_CTL_REF_STD] = sqrt(m2 / (double(n) - 1.0));
+            st[TRLX_CTL_REF_SET] = 1.0;
+        }
+        float d = 0.0f;
+        if (c.scale_mode == TRLX_SCALE_RUNNING) d = float(st[TRLX_CTL_STD]);
+        else if (c.scale_mode == TRLX_SCALE_REF) d = float(st[TRLX_CTL_REF_STD]);
+        s_out[0] = d;
+        s_out[1] = float(st[TRLX_CTL_KL_COEF]);
+        if (writer) {
+#pragma unroll
+            for (int k = 0; k < TRLX_CTL_SLOTS; ++k) c.state_out[k] = st[k];
+        }
+    }
+    __syncthreads();
+    div = s_out[0];
+    beta = s_out[1];
+}
+
+// AdaptiveKLController.update (ppo_models.py:38-44) in fp64 on one thread:
+//   beta *= 1 + clip(current/target - 1, -0.2, 0.2) * n_steps / horizon
+// np.clip propagates NaN, so the clamp is written with comparisons (fmin/fmax would drop it).
+__device__ __forceinline__ void kl_ctl_apply(const KlCtlArgs& k, float approx_kl) {
+    if (!k.state) return;
+    const double cur = double(approx_kl);
+    if (k.adaptive) {
+        double err = cur / k.target - 1.0;
+        err = err < -0.2 ? -0.2 : (err > 0.2 ? 0.2 : err);
+        const double mult = 1.0 + err * k.n_steps / k.horizon;
+        k.state[TRLX_CTL_KL_COEF] = k.state[TRLX_CTL_KL_COEF] * mult;
+    }
+    k.state[TRLX_CTL_KL_UPDATES] += 1.0;
+    k.state[TRLX_CTL_LAST_KL] = cur;
+}
+
+}  // namespace trlx

@@ -12,6 +12,7 @@
 // held its CU slot for a write-through store + returned atomic (~2 us), which cost 10-15%
 // of the streaming kernels' bandwidth (measured) — a separate launch is cheaper.
 #pragma once
+#include "ctl_state.h"
 #include "ppo_math.h"
 
 namespace trlx {
@@ -56,6 +57,8 @@ struct GaeRolloutArgs {
     int ret_dtype;
     double* stats;            // [4] out
     Workspace ws;
+    int has_ctl;              // score/beta control from the device state (ctl_state.h)
+    ScoreCtlArgs ctl;
 };
 
 // KL reward (ppo_orchestrator.py:164-167, score on the last valid column) and GAE
@@ -69,6 +72,20 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
     const int b = blockIdx.x * kRolloutsPerBlock + threadIdx.x / kWave;
     const int T = e.T;
     double s1 = 0.0, s2 = 0.0, sm = 0.0, cnt = 0.0;
+    float neg_beta = e.neg_beta, sdiv = 0.0f, sclip = 0.0f;
+    // Device controller state: with a score scale every block needs the merged statistics
+    // up front (each derives the same values; block 0 stores them).  Without one (the
+    // reference default, scale_reward False) the blocks only read beta and clip, and block 0
+    // advances RunningMoments after its own rollouts, off the other blocks' path.
+    const bool ctl_first = e.has_ctl && e.ctl.scale_mode != TRLX_SCALE_NONE;
+    if (ctl_first) {
+        float beta;
+        score_ctl_block(e.ctl, e.scores, e.B, blockIdx.x == 0, sdiv, beta);
+        neg_beta = -beta;
+    } else if (e.has_ctl) {
+        neg_beta = -float(e.ctl.state_in[TRLX_CTL_KL_COEF]);
+    }
+    if (e.has_ctl) sclip = e.ctl.clip;
     if (b < e.B) {
         const int len = e.lengths ? int(e.lengths[b]) : T;
         const float log2c = e.gl > 0.0f ? __log2f(e.gl) : -INFINITY;
@@ -80,8 +97,8 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
             float v = 0.0f, r = 0.0f;
             if (ok && t < len) {
                 v = ld_any(e.values, e.v_dtype, gi);
-                r = mul_rn(e.neg_beta, e.lp[gi] - e.ref_lp[gi]);
-                if (t == len - 1 && e.scores) r = add_rn(r, e.scores[b]);
+                r = mul_rn(neg_beta, e.lp[gi] - e.ref_lp[gi]);
+                if (t == len - 1 && e.scores) r = add_rn(r, score_transform(e.scores[b], sdiv, sclip));
             }
             float vn = __shfl_down(v, 1, kWave);
             if (lane == kWave - 1) vn = vcarry;
@@ -108,6 +125,10 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
             }
         }
     }
+    if (e.has_ctl && !ctl_first && blockIdx.x == 0) {
+        float d_unused, b_unused;
+        score_ctl_block(e.ctl, e.scores, e.B, true, d_unused, b_unused);
+    }
     const double mine[TRLX_MOMENT_SLOTS] = {s1, s2, cnt, sm};
     const double rec = block_sum_multi<TRLX_MOMENT_SLOTS>(mine, red);
     if (publish_record_last<TRLX_MOMENT_SLOTS>(e.ws.gae_rec + blockIdx.x * TRLX_MOMENT_SLOTS, rec,
@@ -126,6 +147,7 @@ struct LossRolloutArgs {
     float* loss;              // [1] out
     float* stats;             // [13] out
     Workspace ws;
+    KlCtlArgs kl;             // kl_ctl.update(approx_kl) after the stats (state NULL: none)
 };
 
 // Per-token terms of PPOConfig.loss (ppo_models.py:155-178) and d loss / d values for one
@@ -220,7 +242,10 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_loss(LossRolloutArg
             double a[kLossSums];
             for (int k = 0; k < kLossSums; ++k) a[k] = red[k];
             const double msum = L.msum ? *L.msum : double(int64_t(L.B) * L.T);
-            emit_loss_stats(a, double(int64_t(L.B) * L.T), msum, L.vf_coef, L.loss, L.stats);
+            float s13[TRLX_PPO_STATS];
+            emit_loss_stats(a, double(int64_t(L.B) * L.T), msum, L.vf_coef, L.loss, s13);
+            for (int k = 0; k < TRLX_PPO_STATS; ++k) L.stats[k] = s13[k];
+            kl_ctl_apply(L.kl, s13[8]);  // policy/approx_kl
         }
     }
 }

@@ -577,10 +577,10 @@ extern "C" int64_t trlx_ppo_workspace_bytes(int64_t B, int64_t T) {
     return int64_t(carve_workspace(nullptr, B, T, nullptr));
 }
 
-extern "C" int trlx_ppo_rollout_gae(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
-                                    int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
-                                    float kl_coef, float gamma, float lam, float* rewards, float* adv_raw, void* ret,
-                                    int ret_dtype, double* stats, void* workspace, void* stream) {
+static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                            int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                            float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
+                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream) {
     TRLX_REQUIRE(B > 0 && T > 0 && B * T < (1LL << 31), TRLX_ERR_SHAPE, "bad rollout batch %lld x %lld",
                  (long long)B, (long long)T);
     TRLX_REQUIRE(lp && ref_lp && values && rewards && adv_raw && ret && stats && workspace, TRLX_ERR_ARG,
@@ -591,9 +591,38 @@ extern "C" int trlx_ppo_rollout_gae(int64_t B, int64_t T, const float* lp, const
     e.scores = scores; e.lengths = lengths; e.mask = mask; e.neg_beta = -kl_coef; e.gamma = gamma;
     e.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
     e.rewards = rewards; e.adv = adv_raw; e.ret = ret; e.ret_dtype = ret_dtype; e.stats = stats;
+    if (ctl) {
+        TRLX_REQUIRE(scores && ctl->state_in && ctl->state_out, TRLX_ERR_ARG,
+                     "score control needs scores, state_in and state_out");
+        TRLX_REQUIRE(ctl->state_in != ctl->state_out, TRLX_ERR_ARG,
+                     "trlx_ppo_rollout_gae_ctl: state_out must not alias state_in (every block reads it)");
+        TRLX_REQUIRE(ctl->scale_mode >= TRLX_SCALE_NONE && ctl->scale_mode <= TRLX_SCALE_REF, TRLX_ERR_ARG,
+                     "bad scale_mode %d", ctl->scale_mode);
+        e.has_ctl = 1;
+        e.ctl.state_in = ctl->state_in; e.ctl.state_out = ctl->state_out; e.ctl.global_mom = ctl->global_moments;
+        e.ctl.scale_mode = ctl->scale_mode; e.ctl.clip = ctl->cliprange_reward;
+    }
     const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
     hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
     return check_launch("k_rollout_gae");
+}
+
+extern "C" int trlx_ppo_rollout_gae(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                                    int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                                    float kl_coef, float gamma, float lam, float* rewards, float* adv_raw, void* ret,
+                                    int ret_dtype, double* stats, void* workspace, void* stream) {
+    return rollout_gae_impl(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, nullptr, gamma, lam,
+                            rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
+}
+
+extern "C" int trlx_ppo_rollout_gae_ctl(int64_t B, int64_t T, const float* lp, const float* ref_lp,
+                                        const void* values, int v_dtype, const float* scores,
+                                        const int64_t* lengths, const int64_t* mask, const trlx_score_ctl* ctl,
+                                        float gamma, float lam, float* rewards, float* adv_raw, void* ret,
+                                        int ret_dtype, double* stats, void* workspace, void* stream) {
+    TRLX_REQUIRE(ctl, TRLX_ERR_ARG, "NULL trlx_score_ctl");
+    return rollout_gae_impl(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, 0.0f, ctl, gamma, lam,
+                            rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
 }
 
 extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dtype, int64_t B,
@@ -637,17 +666,35 @@ extern "C" int trlx_ppo_loss_rows(const void* logits, int dtype, int64_t B, int6
     return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
 }
 
-extern "C" int trlx_ppo_rollout_loss(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
-                                     float* loss_stats, void* workspace, void* stream) {
+static int rollout_loss_impl(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                             float* loss_stats, void* workspace, const trlx_kl_ctl* kl, void* stream) {
     TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
     TRLX_REQUIRE(loss && loss_stats && workspace, TRLX_ERR_ARG, "NULL argument to trlx_ppo_rollout_loss");
     LossRolloutArgs L = {};
     carve_workspace(workspace, B, T, &L.ws);
     L.B = int(B); L.T = int(T); L.msum = stats ? stats + 3 : nullptr; L.vf_coef = vf_coef; L.loss = loss;
     L.stats = loss_stats;
+    if (kl) {
+        TRLX_REQUIRE(kl->state, TRLX_ERR_ARG, "trlx_kl_ctl.state is NULL");
+        TRLX_REQUIRE(!kl->adaptive || (kl->target != 0.0 && kl->horizon != 0.0), TRLX_ERR_ARG,
+                     "adaptive KL control needs target and horizon");
+        L.kl.state = kl->state; L.kl.adaptive = kl->adaptive; L.kl.target = kl->target;
+        L.kl.horizon = kl->horizon; L.kl.n_steps = double(kl->n_steps);
+    }
     const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
     hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, L);
     return check_launch("k_rollout_loss");
+}
+
+extern "C" int trlx_ppo_rollout_loss(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                                     float* loss_stats, void* workspace, void* stream) {
+    return rollout_loss_impl(B, T, stats, vf_coef, loss, loss_stats, workspace, nullptr, stream);
+}
+
+extern "C" int trlx_ppo_rollout_loss_ctl(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                                         float* loss_stats, void* workspace, const trlx_kl_ctl* kl, void* stream) {
+    TRLX_REQUIRE(kl, TRLX_ERR_ARG, "NULL trlx_kl_ctl");
+    return rollout_loss_impl(B, T, stats, vf_coef, loss, loss_stats, workspace, kl, stream);
 }
 
 extern "C" int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,

@@ -16,6 +16,12 @@ all-reduce between the two halves):
               trlx_ppo_rollout_loss        fixed-order loss sums -> loss + 13 stats
       [optional RCCL all-reduce of the stats vector for logging (reduce_stats=True)]
 
+With `ctl=PPOControlState(...)` the scores pass through the device
+RunningMoments + scale/clip inside the GAE tail and beta is read from / advanced in device
+memory by the two tails (kl_ctl.update(approx_kl) after the loss): still four launches, no
+host synchronisation; under torch.distributed one more 32-B all-reduce (score moments)
+overlaps the experience logits pass.
+
 Buffers (and the zero-filled ticket workspace) are allocated once per shape; a step
 allocates nothing.  Rows (rollouts) are sharded contiguously across ranks by the caller
 (accelerate_ppo_model.py:146-148 semantics); reference-exact loss normalisers stay
@@ -28,6 +34,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .modeling import grad_buffer_like
+from .control import PPOControlState
 from .ppo import PPOConfig
 from .timing import make_event
 
@@ -36,12 +43,14 @@ __all__ = ["PPOHotPath"]
 
 class PPOHotPath:
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
-                 device, kl_coef: float, value_dtype: torch.dtype = torch.float32):
+                 device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
+                 ctl: Optional[PPOControlState] = None):
         self.cfg = cfg
         self.B, self.T, self.V = B, T, V
         self.dtype = logits_dtype
         self.device = torch.device(device)
         self.kl_coef = float(kl_coef)
+        self.ctl = ctl  # device-resident RunningMoments / score clip / KL controller (control.py)
         f32 = dict(dtype=torch.float32, device=self.device)
         self.lp_old = torch.empty((B, T), **f32)
         self.ref_lp = torch.empty((B, T), **f32)
@@ -89,19 +98,28 @@ class PPOHotPath:
             raise ValueError("policy and reference logits must share strides")
         s = torch.cuda.current_stream(self.device)
         B, T, V = self.B, self.T, self.V
+        self.distributed = dist.is_available() and dist.is_initialized()
+        g_mom, work = None, None
+        if self.ctl is not None:  # score moments all-reduce overlaps the logits pass
+            g_mom, work = self.ctl._global_moments(scores, group, async_op=True)
         self._ev("experience", s)
         _lib.call("trlx_lsm_gather_fwd", logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V,
                   logits.stride(0), logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1),
                   self.lp_old.data_ptr(), self.ref_lp.data_ptr(), _lib.F32, None, None, s.cuda_stream)
         self._ev_end("experience", s)
+        if work is not None:
+            work.wait()
         self._ev("rollout_gae", s)
-        _lib.call("trlx_ppo_rollout_gae", B, T, self.lp_old.data_ptr(), self.ref_lp.data_ptr(), old_values.data_ptr(),
-                  _lib.dtype_code(old_values), _lib.ptr(scores), _lib.ptr(lengths), _lib.ptr(mask), self.kl_coef,
-                  float(self.cfg.gamma), float(self.cfg.lam), self.rewards.data_ptr(), self.adv_raw.data_ptr(),
-                  self.returns.data_ptr(), _lib.dtype_code(self.returns), self.adv_stats.data_ptr(),
-                  self.workspace.data_ptr(), s.cuda_stream)
+        tail = (B, T, self.lp_old.data_ptr(), self.ref_lp.data_ptr(), old_values.data_ptr(),
+                _lib.dtype_code(old_values), _lib.ptr(scores), _lib.ptr(lengths), _lib.ptr(mask))
+        outs = (float(self.cfg.gamma), float(self.cfg.lam), self.rewards.data_ptr(), self.adv_raw.data_ptr(),
+                self.returns.data_ptr(), _lib.dtype_code(self.returns), self.adv_stats.data_ptr(),
+                self.workspace.data_ptr(), s.cuda_stream)
+        if self.ctl is not None:
+            _lib.call("trlx_ppo_rollout_gae_ctl", *tail, self.ctl.score_ctl(g_mom), *outs)
+        else:
+            _lib.call("trlx_ppo_rollout_gae", *tail, self.kl_coef, *outs)
         self._ev_end("rollout_gae", s)
-        self.distributed = dist.is_available() and dist.is_initialized()
         if self.distributed:
             dist.all_reduce(self.adv_stats[:3], dist.ReduceOp.SUM, group=group)
         return self.lp_old, self.ref_lp
@@ -126,8 +144,12 @@ class PPOHotPath:
                   self.dvalues.data_ptr(), self.workspace.data_ptr(), s.cuda_stream)
         self._ev_end("loss", s)
         self._ev("rollout_loss", s)
-        _lib.call("trlx_ppo_rollout_loss", B, T, self.adv_stats.data_ptr(), float(self.cfg.vf_coef),
-                  self.loss.data_ptr(), self.stats.data_ptr(), self.workspace.data_ptr(), s.cuda_stream)
+        args = (B, T, self.adv_stats.data_ptr(), float(self.cfg.vf_coef), self.loss.data_ptr(),
+                self.stats.data_ptr(), self.workspace.data_ptr())
+        if self.ctl is not None:  # + kl_ctl.update(approx_kl) (accelerate_ppo_model.py:123,130-131)
+            _lib.call("trlx_ppo_rollout_loss_ctl", *args, self.ctl.kl_ctl(), s.cuda_stream)
+        else:
+            _lib.call("trlx_ppo_rollout_loss", *args, s.cuda_stream)
         self._ev_end("rollout_loss", s)
         return self.loss, self.stats, self.dlogits, self.dvalues
 
