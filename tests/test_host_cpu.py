@@ -133,18 +133,37 @@ def test_dp_whitening_statistics_gloo(golden, world):
         torch.testing.assert_close(w, T(z[f"f32_big/dist{world}/whiten"]), rtol=1e-5, atol=1e-5)
 
 
-def test_ilql_args_layout_matches_header(tmp_path):
-    """The ctypes mirror of trlx_ilql_args has the C compiler's field offsets."""
-    fields = [f[0] for f in _lib.IlqlArgs._fields_]
+@pytest.mark.parametrize("cname,mirror", [("trlx_ilql_args", "IlqlArgs"), ("trlx_score_ctl", "ScoreCtl"),
+                                           ("trlx_kl_ctl", "KlCtl")])
+def test_struct_layout_matches_header(tmp_path, cname, mirror):
+    """The ctypes mirrors of the C-ABI POD structs have the C compiler's field offsets."""
+    cls = getattr(_lib, mirror)
+    fields = [f[0] for f in cls._fields_]
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "trlx_t5_amd.h"\nint main(void){\n'
-                   + "".join(f'printf("%zu\\n", offsetof(trlx_ilql_args, {f}));\n' for f in fields)
-                   + 'printf("%zu\\n", sizeof(trlx_ilql_args));\nreturn 0;}\n')
+                   + "".join(f'printf("%zu\\n", offsetof({cname}, {f}));\n' for f in fields)
+                   + f'printf("%zu\\n", sizeof({cname}));\nreturn 0;}}\n')
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
     got = [int(v) for v in subprocess.check_output([str(exe)]).decode().split()]
-    want = [getattr(_lib.IlqlArgs, f).offset for f in fields] + [__import__("ctypes").sizeof(_lib.IlqlArgs)]
+    want = [getattr(cls, f).offset for f in fields] + [__import__("ctypes").sizeof(cls)]
     assert got == want
+
+
+def test_ctl_slot_constants_match_header():
+    txt = open(HEADER).read()
+    for name in ["SLOTS", "MEAN", "VAR", "STD", "COUNT", "REF_MEAN", "REF_STD", "REF_SET", "KL_COEF", "BATCH_MEAN",
+                 "BATCH_STD", "KL_UPDATES", "LAST_KL"]:
+        m = re.search(rf"#define TRLX_CTL_{name} (\d+)", txt)
+        assert m and int(m.group(1)) == getattr(_lib, f"CTL_{name}"), name
+    for name in ["NONE", "RUNNING", "REF"]:
+        m = re.search(rf"TRLX_SCALE_{name} = (\d+)", txt)
+        assert m and int(m.group(1)) == getattr(_lib, f"SCALE_{name}"), name
+
+
+def test_control_state_refuses_bad_scale():
+    with pytest.raises(ValueError, match="scale_reward"):
+        P.PPOControlState("cpu", scale_reward="bogus")
 
 
 def test_ilql_refuses_cpu_tensors():
