@@ -65,7 +65,9 @@ const char* trlx_last_error(void);
  *   "stream_threads"    workgroup size for streaming rows
  *   "stream_unroll"     16-B loads in flight per thread for streaming rows (2, 4, 8)
  *   "row_order"         resident rows: 0 (default) = step-major vectors, 1 = wave-major
- * Results are identical up to fp32 summation order; only speed changes. */
+ *   "lmhead_dbg"        ping-pong lm_head ablation bits for timing probes ONLY (1 no MFMA,
+ *                       2 no operand DMA, 4 no fragment reads: results are garbage)
+ * Results are identical up to fp32 summation order; only speed changes (except lmhead_dbg). */
 int trlx_set_tuning(const char* key, int64_t value);
 
 /* ---------------------------------------------------------------- A1
@@ -284,13 +286,16 @@ int trlx_ilql_loss_fused(const trlx_ilql_args* args, void* stream);   /* the thr
  * weight: bf16 [V, H] (nn.Linear layout) rows of ldw; H a multiple of 64, rows 16-B
  * aligned.  labels int64 (stride lb; out of range -> NaN).  lp_out [N] of lp_dtype
  * (F32/BF16), lse_out optional fp32 [N].  MFMA (bf16 in, fp32 accumulate) tiles of
- * 128 tokens x 128 vocab with an online max/Σexp epilogue, then a per-token combine.
+ * 256 tokens x 256 vocab (128 x 128 for small N) with an online max/Σexp epilogue, then a
+ * per-token combine.
  * workspace: trlx_lmhead_workspace_bytes(N, V) bytes (no initialisation needed). */
 int64_t trlx_lmhead_workspace_bytes(int64_t N, int64_t V);
-/* Kernel variant (0 = automatic: 256x256 tiles for N >= 2048, else 128x128; 1 persistent
- * 256x256 with 3 stages in flight; 2 256x256 tiles; 3 128x128 tiles; 4 = 2 with an XCD-aware
- * tile order).  Results identical up to fp32 summation order.  Set before sizing the
- * workspace (the vocab tile width changes it). */
+/* Kernel variant (0 = automatic: 8 for N >= 2048, else 3; 1 persistent 256x256 with 3 stages
+ * in flight; 2 256x256 tiles, 2 barriers per K-step; 3 128x128 tiles; 4 = 2 with an XCD-aware
+ * tile order; 5 256x256 ping-pong (two wave groups staggered by a barrier), 4 phases per
+ * K-step; 6 = 5 with the XCD-aware order; 7 persistent ping-pong; 8 ping-pong, 2 phases per
+ * K-step).  Results identical up to fp32 summation order.  Set before sizing the workspace
+ * (the vocab tile width changes it). */
 int trlx_lmhead_set_variant(int variant);
 int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                          int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,

@@ -27,6 +27,9 @@ def timeit(fn, reps=10):
     return sorted(ts)[len(ts) // 2]
 
 
+VARIANTS = tuple(int(v) for v in os.environ.get("LM_VARIANTS", "2,1,5,7,8").split(","))
+
+
 def main():
     dev = torch.device("cuda:0")
     shapes = [("C2 GPT-2 (128x48 tokens)", 6144, 768, 50257), ("C3 T5-base (256x48)", 12288, 768, 32128),
@@ -37,11 +40,14 @@ def main():
         w = (torch.randn(V, H, generator=g, device=dev) * 0.1).to(torch.bfloat16)
         y = torch.randint(0, V, (N,), generator=g, device=dev)
         res = {}
-        for var in (2, 4, 1):
-            P._lib.call("trlx_lmhead_set_variant", var)
-            res[var] = timeit(lambda: P.lm_head_logprobs(h, w, y, out_dtype=torch.float32))
+        for rnd in range(3):  # interleaved rounds (run-to-run drift is several %)
+            for var in VARIANTS:
+                P._lib.call("trlx_lmhead_set_variant", var)
+                res.setdefault(var, []).append(timeit(lambda: P.lm_head_logprobs(h, w, y, out_dtype=torch.float32)))
+        res = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
         P._lib.call("trlx_lmhead_set_variant", 0)
-        fused = min(res.values())
+        res["auto"] = timeit(lambda: P.lm_head_logprobs(h, w, y, out_dtype=torch.float32))
+        fused = res["auto"]
         print("   variants (us):", {k: round(v, 1) for k, v in res.items()})
         gemm = timeit(lambda: h @ w.t())
         logits = h @ w.t()

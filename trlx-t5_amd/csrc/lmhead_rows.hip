@@ -16,6 +16,8 @@
 //
 // The GEMM is MFMA-bound (2·H FLOP per token·vocab pair); the partials cost 8 B per
 // (token, vocab tile) — 1/16 of writing the bf16 logits.
+#include <type_traits>
+
 #include "common.h"
 
 namespace trlx {
@@ -56,6 +58,7 @@ struct LmHeadArgs {
     float* xlab;           // [N] label logit
     int nvt;
     int xcd_swizzle;       // 1: remap blockIdx so each XCD gets a contiguous range of tiles
+    int dbg;               // ping-pong ablation bits (timing probes only; 0 = normal)
 };
 
 // Swizzled LDS image of a [rows][64 k] bf16 tile: row r is 128 B; its 16-B chunk c sits at
@@ -88,6 +91,26 @@ __device__ __forceinline__ void lm_stage(const LmHeadArgs& a, char* stage, int m
         __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(stage + G::BM * 128 + g * 1024),
                                          16, 0, 0);
     }
+}
+
+// All-reduce over each 16-lane DPP row (the 16 columns of a 16x16 MFMA tile row) by four
+// row_ror rotations: VALU-latency DPP instead of LDS-latency ds_bpermute chains.  Every lane
+// ends with the row's value (the sum's association differs per lane; callers use lane 0).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+    v = fmaxf(v, dpp_f<0x128>(v));  // row_ror:8
+    v = fmaxf(v, dpp_f<0x124>(v));  // row_ror:4
+    v = fmaxf(v, dpp_f<0x122>(v));  // row_ror:2
+    return fmaxf(v, dpp_f<0x121>(v));  // row_ror:1
+}
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0x128>(v);
+    v += dpp_f<0x124>(v);
+    v += dpp_f<0x122>(v);
+    return v + dpp_f<0x121>(v);
 }
 
 __device__ __forceinline__ bf16x8_t lds_frag(const char* tile, int r, int c) {
@@ -173,15 +196,13 @@ __global__ __launch_bounds__(G::kThreads) void k_lmhead_tiles(LmHeadArgs a) {
                 x[j] = v < a.V ? acc[i][j][q] : -INFINITY;
                 mx = fmaxf(mx, x[j]);
             }
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+            mx = row16_max(mx);
             // a fully masked row piece (columns >= V) keeps (-inf, 0): exp(-inf - -inf) is NaN
             const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
             float s = 0.f;
 #pragma unroll
             for (int j = 0; j < G::kNR; ++j) s += exp2_fast(fmaf(x[j], kLog2e, ml2e));
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, kWave);
+            s = row16_sum(s);
             if (cl == 0) cmb[wc * G::BM + rt] = make_float2(mx, s);
             const int dy = lab[rt] - (n0 + wc * G::kWCols);
             if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
@@ -353,14 +374,12 @@ __global__ __launch_bounds__(G::kThreads) void k_lmhead_persist(LmHeadArgs a, in
                     xv[j] = v < a.V ? acc[i][j][q] : -INFINITY;
                     mx = fmaxf(mx, xv[j]);
                 }
-#pragma unroll
-                for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+                mx = row16_max(mx);
                 const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
                 float sm = 0.f;
 #pragma unroll
                 for (int j = 0; j < G::kNR; ++j) sm += exp2_fast(fmaf(xv[j], kLog2e, ml2e));
-#pragma unroll
-                for (int off = 1; off < 16; off <<= 1) sm += __shfl_xor(sm, off, kWave);
+                sm = row16_sum(sm);
                 if (cl == 0) lds_store_f2(cmb + wc * G::BM + rt, mx, sm);
             }
         }
@@ -389,6 +408,630 @@ __global__ __launch_bounds__(G::kThreads) void k_lmhead_persist(LmHeadArgs a, in
         }
         // the next tile's epilogue rewrites cmb only after many barriers
     }
+}
+
+// ------------------------------------------------------------------ ping-pong, 4 phases per K-step
+// 256 x 256 tile, 8 waves (2 x 4, 128 x 64 each) split into two groups by wr.  The waves of
+// group 1 start one barrier late, so on every SIMD (one wave of each group) one wave issues
+// its LDS reads and LDS-DMA loads while the other runs MFMAs (cdna_hip_programming.md "The
+// 256² 8-phase template": ping-pong + counted vmcnt + raw barriers).
+//
+// A 64-deep K-step is four phases, one per 64 x 32 quadrant (qm, qn) of the wave's block,
+// serpentine (0,0) (0,1) (1,1) (1,0) so each phase reads only the operand that changes:
+//   q0: A rows qm=0 (8 ds_read_b128) + B cols qn=0 (4)     q1: B cols qn=1 (4)
+//   q2: A rows qm=1 (8)                                      q3: nothing (A qm=1, B qn=0 in registers)
+// and then issues 16 MFMAs (4 row x 2 col tiles x 2 k-substeps).  LDS holds two K-steps as
+// eight 16-KB half-tiles (slot = K-step parity x {HA0, HB0, HB1, HA1}):
+//   HA0 = A tile rows {0..63, 128..191}   (qm = 0 of both wave rows)     first read q0
+//   HB0 = B tile cols {64·wc + 0..31}     (qn = 0 of the four wave cols)  first read q0
+//   HB1 = B tile cols {64·wc + 32..63}                                    first read q1
+//   HA1 = A tile rows {64..127, 192..255}                                 first read q2
+// Half-tile s (K-step s/4, kind s%4 in that order) is issued (2 LDS DMAs per lane) in phase
+// s-6 into the slot of s-8, whose last read was >= 2 phases earlier (WAR), and retired by the
+// `vmcnt(8)` of phase s-2 (every phase waits until s <= ph+2), one barrier before its first
+// reader (RAW: issuer vmcnt, then a barrier the reader passed).  Four half-tiles stay in flight.
+constexpr int kPPHalf = 16384;  // bytes per half-tile: 128 rows x 64 k x 2 B
+constexpr int kPPStageBytes = 8 * kPPHalf;
+constexpr int kPPLds = kPPStageBytes + LmBig::WN * LmBig::BM * 8 + LmBig::BM * 4;
+
+__device__ __forceinline__ void pp_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// vmcnt(2n) for the wave-uniform n in [0, 4]
+__device__ __forceinline__ void pp_wait(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
+// Issue half-tile s: 16 groups of 8 rows x 128 B; wave w issues groups w and w + 8.
+__device__ __forceinline__ void pp_issue(const LmHeadArgs& a, char* smem, int m0, int n0, int s, int wave, int lane) {
+    const int kt = s >> 2, kind = s & 3;
+    char* slot = smem + ((kt & 1) * 4 + kind) * kPPHalf;
+    const int rl = lane >> 3, pc = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int g = i * 8 + wave;
+        const int r = g * 8 + rl;  // local row 0..127
+        const uint16_t* src;
+        if (kind == 0 || kind == 3) {  // A half: tile rows (r>>6)*128 + (kind==3)*64 + (r&63)
+            const int tr = (r >> 6) * 128 + (kind == 3 ? 64 : 0) + (r & 63);
+            const int ma = min(m0 + tr, a.N - 1);
+            src = a.h + int64_t(ma) * a.ldh;
+        } else {  // B half: tile cols (r>>5)*64 + (kind==2)*32 + (r&31)
+            const int tc = (r >> 5) * 64 + (kind == 2 ? 32 : 0) + (r & 31);
+            const int nb = min(n0 + tc, a.V - 1);
+            src = a.w + int64_t(nb) * a.ldw;
+        }
+        src += kt * kLmBK + lds_chunk(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(slot + g * 1024), 16, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(512) void k_lmhead_pingpong(LmHeadArgs a) {
+    typedef LmBig G;
+    __shared__ __attribute__((aligned(16))) char smem[kPPLds];  // ONE LDS object (glds waits)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / G::WN, wc = wave % G::WN;
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    int b = blockIdx.x;
+    if (a.xcd_swizzle) {
+        const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = b % 8;
+        b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+    }
+    const int mt = b % ntt, vt = b / ntt;
+    const int m0 = mt * G::BM, n0 = vt * G::BN;
+    float2* cmb = reinterpret_cast<float2*>(smem + kPPStageBytes);
+    int* lab = reinterpret_cast<int*>(smem + kPPStageBytes + G::WN * G::BM * 8);
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        const int m = m0 + t;
+        lab[t] = m < a.N ? int(a.labels[int64_t(m) * a.lb]) : -1;
+    }
+
+    f32x4_t acc[G::kMR][G::kNR];
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = a.H / kLmBK;
+    const int S = 4 * nk;
+    const int pro = S < 6 ? S : 6;
+    for (int s = 0; s < pro; ++s) pp_issue(a, smem, m0, n0, s, wave, lane);
+    pp_wait(min(4, (pro - 2) > 0 ? pro - 2 : 0));  // half-tiles 0, 1 (K-step 0's q0 operands) retired
+    pp_barrier();  // raw: __syncthreads() would drain the prefetch (lab[] is read after many barriers)
+    if (wr == 1) pp_barrier();                    // group 1 runs one barrier behind
+
+    bf16x8_t af[2][4];     // A fragments of the current qm: [k-substep][row tile]
+    bf16x8_t bfr[2][2][2]; // B fragments: [qn][k-substep][col tile]
+    const int fr = lane & 15, fc = lane >> 4;
+    // One phase of the stream; STEADY: the half-tile issue is in range and vmcnt(8) is exact
+    // (every K-step but the last two), so the body has no bounds logic.
+    auto phase = [&](int kt, auto qc, auto steadyc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        constexpr bool steady = decltype(steadyc)::value;
+        const char* buf = smem + (kt & 1) * 4 * kPPHalf;
+        const int ph = 4 * kt + q;
+        // ---- memory section: fragments of this phase, then one half-tile of the stream
+        if constexpr (q == 0 || q == 2) {
+            if (!(a.dbg & 4)) {
+                const char* At = buf + (q == 0 ? 0 : 3) * kPPHalf;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) af[ks][i] = lds_frag(At, wr * 64 + i * 16 + fr, ks * 4 + fc);
+            }
+        }
+        if constexpr (q == 0 || q == 1) {
+            if (!(a.dbg & 4)) {
+                const char* Bt = buf + (q == 0 ? 1 : 2) * kPPHalf;
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) bfr[q][ks][j] = lds_frag(Bt, wc * 32 + j * 16 + fr, ks * 4 + fc);
+            }
+        }
+        if constexpr (steady) {
+            if (!(a.dbg & 2)) pp_issue(a, smem, m0, n0, ph + 6, wave, lane);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            if (ph + 6 < S && !(a.dbg & 2)) pp_issue(a, smem, m0, n0, ph + 6, wave, lane);
+            const int n = min(ph + 6, S - 1) - (ph + 2);
+            pp_wait(n < 0 ? 0 : (n > 4 ? 4 : n));
+        }
+        pp_barrier();
+        // ---- MFMA section: quadrant (qm, qn) = (0,0) (0,1) (1,1) (1,0)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        constexpr int qm = q >= 2 ? 1 : 0;
+        constexpr int qn = (q == 1 || q == 2) ? 1 : 0;
+        __builtin_amdgcn_s_setprio(1);
+        if (!(a.dbg & 1)) {
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[qm * 4 + i][qn * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            af[ks][i], bfr[qn][ks][j], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+    };
+    typedef std::integral_constant<bool, true> Steady;
+    typedef std::integral_constant<bool, false> Tail;
+    int kt = 0;
+    for (; kt + 2 < nk; ++kt) {
+        phase(kt, std::integral_constant<int, 0>{}, Steady{});
+        phase(kt, std::integral_constant<int, 1>{}, Steady{});
+        phase(kt, std::integral_constant<int, 2>{}, Steady{});
+        phase(kt, std::integral_constant<int, 3>{}, Steady{});
+    }
+    for (; kt < nk; ++kt) {
+        phase(kt, std::integral_constant<int, 0>{}, Tail{});
+        phase(kt, std::integral_constant<int, 1>{}, Tail{});
+        phase(kt, std::integral_constant<int, 2>{}, Tail{});
+        phase(kt, std::integral_constant<int, 3>{}, Tail{});
+    }
+    if (wr == 0) pp_barrier();  // balance group 1's extra barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---- epilogue (as k_lmhead_tiles): per token row, the tile's partial (max, Σexp) and
+    // the label logit.  acc[I][J][r] at lane l = logit(token m0 + wr*128 + I*16 + (l>>4)*4 + r,
+    //                                             vocab n0 + wc*64 + J*16 + (l&15))
+    const int cl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rt = wr * G::kWRows + i * 16 + (lane >> 4) * 4 + q;
+            float x[G::kNR];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) {
+                const int v = n0 + wc * G::kWCols + j * 16 + cl;
+                x[j] = v < a.V ? acc[i][j][q] : -INFINITY;
+                mx = fmaxf(mx, x[j]);
+            }
+            mx = row16_max(mx);
+            const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) sm += exp2_fast(fmaf(x[j], kLog2e, ml2e));
+            sm = row16_sum(sm);
+            if (cl == 0) cmb[wc * G::BM + rt] = make_float2(mx, sm);
+            const int dy = lab[rt] - (n0 + wc * G::kWCols);
+            if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+                float xy = x[0];
+#pragma unroll
+                for (int j = 1; j < G::kNR; ++j) xy = (dy >> 4) == j ? x[j] : xy;
+                a.xlab[m0 + rt] = xy;
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        if (m0 + t >= a.N) continue;
+        float m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < G::WN; ++c) m = fmaxf(m, cmb[c * G::BM + t].x);
+        float sm = 0.f;
+        if (m != -INFINITY) {
+#pragma unroll
+            for (int c = 0; c < G::WN; ++c) {
+                const float2 p = cmb[c * G::BM + t];
+                sm += p.x == -INFINITY ? 0.f : p.y * exp2_fast((p.x - m) * kLog2e);
+            }
+        }
+        a.part[int64_t(m0 + t) * a.nvt + vt] = make_float2(m, sm);
+    }
+}
+
+// ------------------------------------------------------------------ ping-pong, 2 phases per K-step
+// As k_lmhead_pingpong with half the barriers: 32 MFMAs per phase (a 64 x 64 half of the
+// wave's block).  Phase 2t reads HA0(t), HB0(t), HB1(t) and computes rows qm = 0; phase 2t+1
+// reads HA1(t) and computes rows qm = 1.  Stream: phase 2u issues HA0/HB0/HB1 of K-step u+1
+// (their slots were last read in phase 2u-2) and waits for HA1(u) (vmcnt(6)); phase 2u+1
+// issues HA1(u+1) (slot last read in 2u-1) and waits for K-step u+1's first three (vmcnt(2)).
+__global__ __launch_bounds__(512) void k_lmhead_pp2(LmHeadArgs a) {
+    typedef LmBig G;
+    __shared__ __attribute__((aligned(16))) char smem[kPPLds];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / G::WN, wc = wave % G::WN;
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    int b = blockIdx.x;
+    if (a.xcd_swizzle) {
+        const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = b % 8;
+        b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+    }
+    const int mt = b % ntt, vt = b / ntt;
+    const int m0 = mt * G::BM, n0 = vt * G::BN;
+    float2* cmb = reinterpret_cast<float2*>(smem + kPPStageBytes);
+    int* lab = reinterpret_cast<int*>(smem + kPPStageBytes + G::WN * G::BM * 8);
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        const int m = m0 + t;
+        lab[t] = m < a.N ? int(a.labels[int64_t(m) * a.lb]) : -1;
+    }
+    f32x4_t acc[G::kMR][G::kNR];
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int nk = a.H / kLmBK;
+    // K-step 0: all four half-tiles; wait for HA0/HB0/HB1 (HA1 may stay in flight)
+#pragma unroll
+    for (int kind = 0; kind < 4; ++kind) pp_issue(a, smem, m0, n0, kind, wave, lane);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    pp_barrier();
+    if (wr == 1) pp_barrier();
+    if ((a.dbg & 8) && wr == 1) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
+    bf16x8_t af[2][4];
+    bf16x8_t bfr[2][2][2];
+    const int fr = lane & 15, fc = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* buf = smem + (kt & 1) * 4 * kPPHalf;
+        const bool more = kt + 1 < nk;
+        // ---- phase 2kt: rows qm = 0
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[ks][i] = lds_frag(buf, wr * 64 + i * 16 + fr, ks * 4 + fc);
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    bfr[qn][ks][j] = lds_frag(buf + (1 + qn) * kPPHalf, wc * 32 + j * 16 + fr, ks * 4 + fc);
+        if (more && !(a.dbg & 2)) {
+            pp_issue(a, smem, m0, n0, 4 * (kt + 1) + 0, wave, lane);
+            pp_issue(a, smem, m0, n0, 4 * (kt + 1) + 1, wave, lane);
+            pp_issue(a, smem, m0, n0, 4 * (kt + 1) + 2, wave, lane);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // HA1(kt) landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        pp_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (!(a.dbg & 24)) __builtin_amdgcn_s_setprio(1);
+        if (!(a.dbg & 1))
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][qn * 2 + j] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[qn][ks][j], acc[i][qn * 2 + j], 0, 0, 0);
+        if (!(a.dbg & 24)) __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+        // ---- phase 2kt+1: rows qm = 1
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                af[ks][i] = lds_frag(buf + 3 * kPPHalf, wr * 64 + i * 16 + fr, ks * 4 + fc);
+        if (more && !(a.dbg & 2)) {
+            pp_issue(a, smem, m0, n0, 4 * (kt + 1) + 3, wave, lane);
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // K-step kt+1's HA0/HB0/HB1 landed
+        }
+        pp_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (!(a.dbg & 24)) __builtin_amdgcn_s_setprio(1);
+        if (!(a.dbg & 1))
+#pragma unroll
+        for (int qn = 1; qn >= 0; --qn)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[4 + i][qn * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[qn][ks][j],
+                                                                                        acc[4 + i][qn * 2 + j], 0, 0, 0);
+        if (!(a.dbg & 24)) __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+    }
+    if (wr == 0) pp_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rt = wr * G::kWRows + i * 16 + (lane >> 4) * 4 + q;
+            float x[G::kNR];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) {
+                const int v = n0 + wc * G::kWCols + j * 16 + cl;
+                x[j] = v < a.V ? acc[i][j][q] : -INFINITY;
+                mx = fmaxf(mx, x[j]);
+            }
+            mx = row16_max(mx);
+            const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) sm += exp2_fast(fmaf(x[j], kLog2e, ml2e));
+            sm = row16_sum(sm);
+            if (cl == 0) cmb[wc * G::BM + rt] = make_float2(mx, sm);
+            const int dy = lab[rt] - (n0 + wc * G::kWCols);
+            if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+                float xy = x[0];
+#pragma unroll
+                for (int j = 1; j < G::kNR; ++j) xy = (dy >> 4) == j ? x[j] : xy;
+                a.xlab[m0 + rt] = xy;
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        if (m0 + t >= a.N) continue;
+        float m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < G::WN; ++c) m = fmaxf(m, cmb[c * G::BM + t].x);
+        float sm = 0.f;
+        if (m != -INFINITY) {
+#pragma unroll
+            for (int c = 0; c < G::WN; ++c) {
+                const float2 p = cmb[c * G::BM + t];
+                sm += p.x == -INFINITY ? 0.f : p.y * exp2_fast((p.x - m) * kLog2e);
+            }
+        }
+        a.part[int64_t(m0 + t) * a.nvt + vt] = make_float2(m, sm);
+    }
+}
+
+// ------------------------------------------------------------------ persistent ping-pong
+// k_lmhead_pingpong's schedule as ONE stream over all of a workgroup's tiles (tile j of
+// workgroup b is b + j·gridDim): the half-tile stream, its slots (parity of the GLOBAL
+// K-step count) and the counted waits run straight across tile boundaries, so a tile's
+// first operands are already in LDS when its predecessor's last MFMAs retire.  Per tile:
+//   * its labels (low dwords, 2 KB) arrive by LDS DMA issued just before the tile's first
+//     half-tile, into a label buffer of the tile's parity (an ordinary load would make hipcc
+//     drain the DMA queue; the extra DMA only makes later counted waits more conservative:
+//     vector-memory ops retire in issue order);
+//   * the epilogue is per wave group: the four waves of a wave row own the same 128 token
+//     rows, so a group publishes its (max, Σexp) partials to LDS, passes ONE barrier and
+//     merges them — group 0's epilogue runs beside group 1's last MFMA phase.
+constexpr int kPPLabOff = kPPStageBytes + LmBig::WN * LmBig::BM * 8;  // int32 [2][256]
+constexpr int kPPLabRing = 4;  // label buffers: tile j+4's DMA is issued after tile j's epilogue even at H = 64
+constexpr int kPP2Lds = kPPLabOff + kPPLabRing * LmBig::BM * 4;
+
+__device__ __forceinline__ void pp2_issue(const LmHeadArgs& a, char* smem, int m0, int n0, int kt, int kind,
+                                          int parity, int wave, int lane) {
+    char* slot = smem + (parity * 4 + kind) * kPPHalf;
+    const int rl = lane >> 3, pc = lane & 7;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int g = i * 8 + wave;
+        const int r = g * 8 + rl;
+        const uint16_t* src;
+        if (kind == 0 || kind == 3) {
+            const int tr = (r >> 6) * 128 + (kind == 3 ? 64 : 0) + (r & 63);
+            src = a.h + int64_t(min(m0 + tr, a.N - 1)) * a.ldh;
+        } else {
+            const int tc = (r >> 5) * 64 + (kind == 2 ? 32 : 0) + (r & 31);
+            src = a.w + int64_t(min(n0 + tc, a.V - 1)) * a.ldw;
+        }
+        src += kt * kLmBK + lds_chunk(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(slot + g * 1024), 16, 0, 0);
+    }
+}
+
+// Labels of the tile at m0 -> int32 lab[parity][256] (waves 0-3: 64 rows each).
+__device__ __forceinline__ void pp2_issue_labels(const LmHeadArgs& a, char* smem, int m0, int parity, int wave,
+                                                 int lane) {
+    if (wave >= 4) return;
+    const int r = wave * 64 + lane;
+    const int64_t* src = a.labels + int64_t(min(m0 + r, a.N - 1)) * a.lb;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + kPPLabOff +
+                                                                                    parity * 1024 + wave * 256),
+                                     4, 0, 0);
+}
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t lds_load_i4(const int* p) {
+    const uint32_t addr = uint32_t(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const int*)p));
+    i32x4_t v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+
+__global__ __launch_bounds__(512) void k_lmhead_pp_persist(LmHeadArgs a, int ntiles) {
+    typedef LmBig G;
+    __shared__ __attribute__((aligned(16))) char smem[kPP2Lds];  // ONE LDS object (glds waits)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / G::WN, wc = wave % G::WN;
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    const int nk = a.H / kLmBK;
+    const int mine = (ntiles - int(blockIdx.x) + int(gridDim.x) - 1) / int(gridDim.x);
+    if (mine <= 0) return;
+    const int SK = mine * nk;  // K-steps in this workgroup's stream
+    const int S = 4 * SK;      // half-tiles (= phases)
+    float2* cmb = reinterpret_cast<float2*>(smem + kPPStageBytes);
+    const int* labs = reinterpret_cast<const int*>(smem + kPPLabOff);
+
+    auto tile_origin = [&](int j, int& m0, int& n0) {
+        const int t = int(blockIdx.x) + j * int(gridDim.x);
+        m0 = (t % ntt) * G::BM;
+        n0 = (t / ntt) * G::BN;
+    };
+    // Issue targets run 1-2 K-steps ahead of consumption, so they lie in the current tile or
+    // the next one: both origins are kept as wave-uniform scalars (no per-issue division).
+    int cm0, cn0, xm0, xn0;  // current tile j / next tile j+1
+    tile_origin(0, cm0, cn0);
+    tile_origin(1, xm0, xn0);
+    // half-tile `kind` of K-step kt + d of tile j (d in {0, 1, 2}); g = global K-step index
+    auto issue_at = [&](int j, int kt, int d, int kind, int g) __attribute__((always_inline)) {
+        if (a.dbg & 2) return;
+        int t_kt = kt + d, m0 = cm0, n0 = cn0, jj = j;
+        if (t_kt >= nk) {
+            t_kt -= nk;
+            m0 = xm0;
+            n0 = xn0;
+            jj = j + 1;
+        }
+        if (t_kt == 0 && kind == 0) pp2_issue_labels(a, smem, m0, jj % kPPLabRing, wave, lane);
+        pp2_issue(a, smem, m0, n0, t_kt, kind, (g + d) & 1, wave, lane);
+    };
+
+    f32x4_t acc[G::kMR][G::kNR];
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int s2 = 0; s2 < 6; ++s2) issue_at(0, 0, s2 >> 2, s2 & 3, 0);  // K-steps 0 and 1 (1: maybe tile 1)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-step 0's q0 operands (+ tile 0 labels) landed
+    pp_barrier();
+    if (wr == 1) pp_barrier();  // group 1 runs one barrier behind
+
+    bf16x8_t af[2][4];
+    bf16x8_t bfr[2][2][2];
+    const int fr = lane & 15, fc = lane >> 4;
+
+    auto phase = [&](int j, int kt, int g, auto qc, auto steadyc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        constexpr bool steady = decltype(steadyc)::value;
+        const char* buf = smem + (g & 1) * 4 * kPPHalf;
+        const int ph = 4 * g + q;
+        // issue target: half-tile ph + 6 = K-step g + 1 (kinds 2, 3) or g + 2 (kinds 0, 1)
+        constexpr int d = q < 2 ? 1 : 2;
+        constexpr int kind = (q + 2) & 3;
+        if constexpr (q == 0 || q == 2) {
+            if (!(a.dbg & 4)) {
+            const char* At = buf + (q == 0 ? 0 : 3) * kPPHalf;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[ks][i] = lds_frag(At, wr * 64 + i * 16 + fr, ks * 4 + fc);
+            }
+        }
+        if constexpr (q == 0 || q == 1) {
+            if (!(a.dbg & 4)) {
+            const char* Bt = buf + (q == 0 ? 1 : 2) * kPPHalf;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) bfr[q][ks][j] = lds_frag(Bt, wc * 32 + j * 16 + fr, ks * 4 + fc);
+            }
+        }
+        if constexpr (steady) {
+            issue_at(j, kt, d, kind, g);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            if (ph + 6 < S) issue_at(j, kt, d, kind, g);
+            const int n = min(ph + 6, S - 1) - (ph + 2);
+            pp_wait(n < 0 ? 0 : (n > 4 ? 4 : n));
+        }
+        pp_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        constexpr int qm = q >= 2 ? 1 : 0;
+        constexpr int qn = (q == 1 || q == 2) ? 1 : 0;
+        __builtin_amdgcn_s_setprio(1);
+        if (!(a.dbg & 1))
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[qm * 4 + i][qn * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        af[ks][i], bfr[qn][ks][j], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+    };
+
+    typedef std::integral_constant<bool, true> Steady;
+    for (int j = 0; j < mine; ++j) {
+        for (int kt = 0; kt < nk; ++kt) {
+            const int g = j * nk + kt;
+            // every phase is "steady": past the end of the stream the issues fetch clamped,
+            // never-read rows of a phantom tile, so vmcnt(8) is exact throughout
+            phase(j, kt, g, std::integral_constant<int, 0>{}, Steady{});
+            phase(j, kt, g, std::integral_constant<int, 1>{}, Steady{});
+            phase(j, kt, g, std::integral_constant<int, 2>{}, Steady{});
+            phase(j, kt, g, std::integral_constant<int, 3>{}, Steady{});
+        }
+        // ---- tile epilogue, per wave group (see above).  acc[I][J][r] at lane l =
+        // logit(token m0 + wr*128 + I*16 + (l>>4)*4 + r, vocab n0 + wc*64 + J*16 + (l&15))
+        const int m0 = cm0, n0 = cn0;
+        const int vt = n0 / G::BN;
+        const int* lab = labs + (j % kPPLabRing) * G::BM;
+        // lane-derived bases laundered here: otherwise hipcc hoists the 32 row addresses out
+        // of the tile loop and spills them, and the scratch reloads wait vmcnt(0) (draining
+        // the operand stream at every tile boundary)
+        const int cl = launder_int(lane & 15);
+        const int rbase = launder_int(wr * G::kWRows + (lane >> 4) * 4);
+        float2* cmbw = cmb + launder_int(wc * G::BM);
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i) {
+            const i32x4_t lab4 = lds_load_i4(lab + rbase + i * 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rt = rbase + i * 16 + q;
+                float x[G::kNR];
+                float mx = -INFINITY;
+#pragma unroll
+                for (int jj = 0; jj < G::kNR; ++jj) {
+                    const int v = n0 + wc * G::kWCols + jj * 16 + cl;
+                    x[jj] = v < a.V ? acc[i][jj][q] : -INFINITY;
+                    mx = fmaxf(mx, x[jj]);
+                }
+                mx = row16_max(mx);
+                const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
+                float sm = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < G::kNR; ++jj) sm += exp2_fast(fmaf(x[jj], kLog2e, ml2e));
+                sm = row16_sum(sm);
+                if (cl == 0) lds_store_f2(cmbw + rt, mx, sm);
+                const int dy = lab4[q] - (n0 + wc * G::kWCols);
+                if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+                    float xy = x[0];
+#pragma unroll
+                    for (int jj = 1; jj < G::kNR; ++jj) xy = (dy >> 4) == jj ? x[jj] : xy;
+                    a.xlab[m0 + rt] = xy;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+            for (int jj = 0; jj < G::kNR; ++jj) acc[i][jj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();  // the group's four waves published their partials
+        {
+            const int gt = tid - wr * 256;  // 0..255 within the group; rows wr*128 + [0, 128)
+            if (gt < 128 && m0 + wr * 128 + gt < a.N) {
+                const int r = wr * 128 + gt;
+                float2 pw[G::WN];
+                float m = -INFINITY;
+#pragma unroll
+                for (int c2 = 0; c2 < G::WN; ++c2) {
+                    pw[c2] = lds_load_f2(cmb + c2 * G::BM + r);
+                    m = fmaxf(m, pw[c2].x);
+                }
+                float sm = 0.f;
+                if (m != -INFINITY) {
+#pragma unroll
+                    for (int c2 = 0; c2 < G::WN; ++c2)
+                        sm += pw[c2].x == -INFINITY ? 0.f : pw[c2].y * exp2_fast((pw[c2].x - m) * kLog2e);
+                }
+                a.part[int64_t(m0 + r) * a.nvt + vt] = make_float2(m, sm);
+            }
+        }
+        cm0 = xm0;
+        cn0 = xn0;
+        tile_origin(j + 2, xm0, xn0);
+    }
+    if (wr == 0) pp_barrier();  // balance group 1's extra barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // One wave per token: merge the nvt partials (fixed order per lane, then a fixed butterfly).
@@ -444,21 +1087,27 @@ __global__ __launch_bounds__(256) void k_lmhead_combine(LmHeadArgs a, void* lp, 
 using namespace trlx;
 
 // variant: 0 auto, 1 persistent 256x256 (BK 32, 3 stages in flight), 2 256x256 tiles, 3 128x128
-// tiles, 4 = 2 with the XCD remap
-// auto (measured on MI355X, tools/lmhead_bench.py): short K (H <= 1024, a tile is <= 32 K-steps)
-// -> persistent, which hides each tile's operand-fetch latency behind the previous tile;
-// long K -> the plain 256x256 tiles; small N -> 128x128 tiles (enough workgroups).
+// tiles, 4 = 2 with the XCD remap, 5 ping-pong 4 phases per K-step, 6 = 5 with the XCD remap,
+// 7 persistent ping-pong, 8 ping-pong 2 phases per K-step.
+// auto (measured on MI355X, tools/lmhead_bench.py, interleaved rounds): N >= 2048 -> 8 (the
+// fastest at every BASELINE shape: 1.1-1.4x the 2-barrier tiles); small N -> 128x128 tiles
+// (enough workgroups to fill 256 CUs).
 static int g_lm_variant = 0;
+static int g_lm_dbg = 0;  // ping-pong ablation bits, set via trlx_set_tuning("lmhead_dbg") (timing probes)
 static int lm_variant(int64_t N, int64_t H = 0) {
+    (void)H;
     if (g_lm_variant) return g_lm_variant;
-    if (N < 2048) return 3;
-    return H <= 1024 ? 1 : 2;
+    return N < 2048 ? 3 : 8;
 }
 static int lm_tile_n(int64_t N) { return lm_variant(N) == 3 ? LmSmall::BN : LmBig::BN; }
 static_assert(LmSmall::BN == 128 && LmBig::BN == 256, "tile widths");
 
+namespace trlx {
+void lm_set_dbg(int v) { g_lm_dbg = v; }
+}  // namespace trlx
+
 extern "C" int trlx_lmhead_set_variant(int v) {
-    TRLX_REQUIRE(v >= 0 && v <= 4, TRLX_ERR_ARG, "lmhead variant 0..4");
+    TRLX_REQUIRE(v >= 0 && v <= 8, TRLX_ERR_ARG, "lmhead variant 0..8");
     g_lm_variant = v;
     return TRLX_OK;
 }
@@ -498,6 +1147,28 @@ static int lm_launch(const LmHeadArgs& a, hipStream_t stream) {
     return check_launch("k_lmhead_tiles");
 }
 
+static int lm_launch_pp_persist(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntiles = int64_t((a.N + LmBig::BM - 1) / LmBig::BM) * a.nvt;
+    TRLX_REQUIRE(ntiles < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    const int grid = int(ntiles < lm_num_cus() ? ntiles : lm_num_cus());
+    hipLaunchKernelGGL(k_lmhead_pp_persist, dim3(grid), dim3(512), 0, stream, a, int(ntiles));
+    return check_launch("k_lmhead_pp_persist");
+}
+
+static int lm_launch_pp2(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntt = (a.N + LmBig::BM - 1) / LmBig::BM;
+    TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    hipLaunchKernelGGL(k_lmhead_pp2, dim3(unsigned(ntt * a.nvt)), dim3(512), 0, stream, a);
+    return check_launch("k_lmhead_pp2");
+}
+
+static int lm_launch_pingpong(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntt = (a.N + LmBig::BM - 1) / LmBig::BM;
+    TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    hipLaunchKernelGGL(k_lmhead_pingpong, dim3(unsigned(ntt * a.nvt)), dim3(512), 0, stream, a);
+    return check_launch("k_lmhead_pingpong");
+}
+
 extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                                     int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
                                     int lp_dtype, float* lse_out, void* workspace, void* stream) {
@@ -527,8 +1198,12 @@ extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void*
     a.part = static_cast<float2*>(workspace);
     a.xlab = reinterpret_cast<float*>(static_cast<char*>(workspace) + N * a.nvt * int64_t(sizeof(float2)));
     const int var = lm_variant(N, H);
-    a.xcd_swizzle = var == 4;
-    int rc = var == 1              ? lm_launch_persist<LmBig>(a, (hipStream_t)stream)
+    a.xcd_swizzle = var == 4 || var == 6;
+    a.dbg = g_lm_dbg;
+    int rc = var == 8              ? lm_launch_pp2(a, (hipStream_t)stream)
+             : var == 7            ? lm_launch_pp_persist(a, (hipStream_t)stream)
+             : var == 5 || var == 6 ? lm_launch_pingpong(a, (hipStream_t)stream)
+             : var == 1            ? lm_launch_persist<LmBig>(a, (hipStream_t)stream)
              : var == 2 || var == 4 ? lm_launch<LmBig>(a, (hipStream_t)stream)
                                     : lm_launch<LmSmall>(a, (hipStream_t)stream);
     if (rc) return rc;
