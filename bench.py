@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--host-state", action="store_true",
                    help="PPO: keep beta as a host constant and skip the score RunningMoments/clip and the KL "
                         "controller update (the default runs them on device, ppo_config.yml settings)")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="PPO: run the loss tail on the main stream (default: side stream, beside the next step's "
+                        "experience rows)")
     p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -225,7 +228,7 @@ def main():
         x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked)
         cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
         ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
-        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl)
+        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap)
 
         def step():
             return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],

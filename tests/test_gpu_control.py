@@ -188,3 +188,28 @@ def test_hot_path_device_state_needs_no_host_sync():
     after = c.host()
     assert after["count"] == pytest.approx(before["count"] + 2 * B)
     assert after["kl_updates"] == before["kl_updates"] + 2
+
+
+def test_overlapped_loss_tail_matches_serial():
+    """overlap_tail=True (the loss tail on a side stream beside the next step's experience
+    rows) gives bit-identical losses, stats, gradients and controller state over several
+    steps; stats are read after wait_stats()."""
+    B, Tn, V = 16, 33, 3001
+    outs = {}
+    for overlap in (False, True):
+        cfg = P.PPOConfig(scale_reward="running")
+        c = P.PPOControlState.from_config(cfg, DEV, n_steps=B)
+        hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.0, ctl=c, overlap_tail=overlap)
+        g = torch.Generator().manual_seed(2)
+        rec = []
+        for step in range(4):
+            logits, ref_logits, new_logits, labels, old_values, values = [cuda(t) for t in _step_inputs(B, Tn, V, step)]
+            scores = cuda(torch.randn(B, generator=g) * 9)
+            loss, stats, dl, dv = hp.step(logits, ref_logits, new_logits, labels, old_values, values, scores)
+            hp.wait_stats()
+            rec.append((loss.clone(), stats.clone(), dl.clone(), dv.clone(), c.state.clone()))
+        torch.cuda.synchronize()
+        outs[overlap] = rec
+    for a, b in zip(outs[False], outs[True]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)

@@ -36,7 +36,7 @@ from . import _lib
 from .modeling import grad_buffer_like
 from .control import PPOControlState
 from .ppo import PPOConfig
-from .timing import make_event
+from .timing import LaunchEvent, make_event
 
 __all__ = ["PPOHotPath"]
 
@@ -44,13 +44,22 @@ __all__ = ["PPOHotPath"]
 class PPOHotPath:
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
                  device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
-                 ctl: Optional[PPOControlState] = None):
+                 ctl: Optional[PPOControlState] = None, overlap_tail: bool = False):
         self.cfg = cfg
         self.B, self.T, self.V = B, T, V
         self.dtype = logits_dtype
         self.device = torch.device(device)
         self.kl_coef = float(kl_coef)
         self.ctl = ctl  # device-resident RunningMoments / score clip / KL controller (control.py)
+        # overlap_tail: the latency-bound loss tail runs on a side stream, beside the NEXT
+        # step's experience rows (it only reads the token records and Σmask, which nothing
+        # before the next GAE tail rewrites); loss / stats are ready at `tail_done`.
+        self.tail_stream = torch.cuda.Stream(self.device) if overlap_tail else None
+        self.tail_done = None
+        # fence-free events (timing.LaunchEvent), two of each reused alternately: a default
+        # event's system-scope fence on record idles the queue for microseconds
+        self._sync_events = [LaunchEvent() for _ in range(4)] if overlap_tail else None
+        self._sync_i = 0
         f32 = dict(dtype=torch.float32, device=self.device)
         self.lp_old = torch.empty((B, T), **f32)
         self.ref_lp = torch.empty((B, T), **f32)
@@ -109,6 +118,8 @@ class PPOHotPath:
         self._ev_end("experience", s)
         if work is not None:
             work.wait()
+        if self.tail_done is not None:  # previous loss tail: reads adv_stats[3] + token records, updates beta
+            self.tail_done.wait(s)
         self._ev("rollout_gae", s)
         tail = (B, T, self.lp_old.data_ptr(), self.ref_lp.data_ptr(), old_values.data_ptr(),
                 _lib.dtype_code(old_values), _lib.ptr(scores), _lib.ptr(lengths), _lib.ptr(mask))
@@ -143,15 +154,35 @@ class PPOHotPath:
                   float(self.cfg.vf_coef), self.lp_new.data_ptr(), dx.data_ptr(), dx.stride(0), dx.stride(1),
                   self.dvalues.data_ptr(), self.workspace.data_ptr(), s.cuda_stream)
         self._ev_end("loss", s)
-        self._ev("rollout_loss", s)
+        ts = s
+        if self.tail_stream is not None:
+            rows_done = self._next_event()
+            rows_done.record(s)
+            ts = self.tail_stream
+            rows_done.wait(ts)
+        self._ev("rollout_loss", ts)
         args = (B, T, self.adv_stats.data_ptr(), float(self.cfg.vf_coef), self.loss.data_ptr(),
                 self.stats.data_ptr(), self.workspace.data_ptr())
         if self.ctl is not None:  # + kl_ctl.update(approx_kl) (accelerate_ppo_model.py:123,130-131)
-            _lib.call("trlx_ppo_rollout_loss_ctl", *args, self.ctl.kl_ctl(), s.cuda_stream)
+            _lib.call("trlx_ppo_rollout_loss_ctl", *args, self.ctl.kl_ctl(), ts.cuda_stream)
         else:
-            _lib.call("trlx_ppo_rollout_loss", *args, s.cuda_stream)
-        self._ev_end("rollout_loss", s)
+            _lib.call("trlx_ppo_rollout_loss", *args, ts.cuda_stream)
+        self._ev_end("rollout_loss", ts)
+        if self.tail_stream is not None:
+            self.tail_done = self._next_event()
+            self.tail_done.record(ts)
         return self.loss, self.stats, self.dlogits, self.dvalues
+
+    def wait_stats(self, stream=None):
+        """Make `stream` (default: the current one) wait for the loss / stats of the last
+        step (a no-op unless overlap_tail)."""
+        if self.tail_done is not None:
+            self.tail_done.wait(stream or torch.cuda.current_stream(self.device))
+
+    def _next_event(self):
+        ev = self._sync_events[self._sync_i]
+        self._sync_i = (self._sync_i + 1) % len(self._sync_events)
+        return ev
 
     def step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
              lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None,
@@ -165,6 +196,7 @@ class PPOHotPath:
         self.experience(logits, ref_logits, labels, old_values, scores, lengths=lengths, mask=mask, group=group)
         out = self.policy_loss(new_logits, labels, values, old_values, mask=mask)
         if reduce_stats and self.distributed:
+            self.wait_stats()
             dist.all_reduce(self.stats, dist.ReduceOp.SUM, group=group)  # logging: mean over ranks
             self.stats.div_(dist.get_world_size(group))
         return out

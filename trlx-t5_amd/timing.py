@@ -26,8 +26,9 @@ def _runtime():
         lib.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
         lib.hipEventSynchronize.argtypes = [ctypes.c_void_p]
         lib.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        lib.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
         for f in ("hipEventCreateWithFlags", "hipEventRecord", "hipEventElapsedTime", "hipEventSynchronize",
-                  "hipEventDestroy"):
+                  "hipEventDestroy", "hipStreamWaitEvent"):
             getattr(lib, f).restype = ctypes.c_int
         _hip = lib
     return _hip
@@ -60,6 +61,11 @@ class LaunchEvent:
     def record(self, stream):
         """stream: a torch.cuda.Stream (its raw hipStream_t is used)."""
         _check(_runtime().hipEventRecord(self._ev, ctypes.c_void_p(stream.cuda_stream)), "hipEventRecord")
+
+    def wait(self, stream):
+        """Make `stream` wait for this event (cross-stream ordering on one device; the kernels'
+        own dispatch acquire / end-of-kernel release make the data visible)."""
+        _check(_runtime().hipStreamWaitEvent(ctypes.c_void_p(stream.cuda_stream), self._ev, 0), "hipStreamWaitEvent")
 
     def elapsed_time(self, end: "LaunchEvent") -> float:
         """Milliseconds between this event and `end` (waits for `end`)."""
