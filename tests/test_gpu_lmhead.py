@@ -84,7 +84,7 @@ def test_lmhead_c2_shape_rows_and_determinism():
     torch.testing.assert_close(lp1[rows.to(DEV)].cpu().double(), want, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_lmhead_every_variant_vs_oracle(variant):
     """Every tile kernel (1 persistent, 2/4 256x256 tiles, 3 128x128, 5/6 ping-pong 256x256, 7 persistent
     ping-pong)

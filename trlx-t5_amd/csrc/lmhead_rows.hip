@@ -787,6 +787,159 @@ __global__ __launch_bounds__(512) void k_lmhead_pp2(LmHeadArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ ping-pong, 32-deep K-steps, 4-slot ring
+// The 2-phase schedule's MFMA : barrier ratio with a deeper operand stream: a K-step is 32
+// deep (32 KB of A + B), LDS holds a ring of four, and each phase consumes one K-step with
+// 32 MFMAs per wave (12 fragment reads: 8 A row tiles, 4 B column tiles).  Phase t issues
+// K-step t+3 into the slot of t-1 and waits (vmcnt(8)) for K-step t+1, so every operand has
+// two phases to land.  WAR: the reading group retires its fragment reads (lgkmcnt(0)) before
+// the barrier that ends its memory section, so a slot is free for DMA right after it.
+constexpr int kP9BK = 32;
+constexpr int kP9Slot = (LmBig::BM + LmBig::BN) * kP9BK * 2;  // 32 KB
+constexpr int kP9LabOff = 4 * kP9Slot + LmBig::WN * LmBig::BM * 8;
+constexpr int kP9Lds = kP9LabOff + LmBig::BM * 4;
+
+// K-step kt (32 deep) -> ring slot kt & 3: A then B, 1-KB groups of 16 rows x 64 B; wave w
+// issues A groups w, w+8 and B groups w, w+8 (4 DMAs per lane).
+__device__ __forceinline__ void p9_issue(const LmHeadArgs& a, char* smem, int m0, int n0, int kt, int wave, int lane) {
+    char* slot = smem + (kt & 3) * kP9Slot;
+    const int rl = lane >> 2, pc = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int g = i * 8 + wave;
+        const int r = g * 16 + rl;
+        const uint16_t* src = a.h + int64_t(min(m0 + r, a.N - 1)) * a.ldh + kt * kP9BK + lds_chunk64(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(slot + g * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int g = i * 8 + wave;
+        const int r = g * 16 + rl;
+        const uint16_t* src = a.w + int64_t(min(n0 + r, a.V - 1)) * a.ldw + kt * kP9BK + lds_chunk64(r, pc) * 8;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(slot + LmBig::BM * 64 + g * 1024),
+                                         16, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(512) void k_lmhead_pp9(LmHeadArgs a) {
+    typedef LmBig G;
+    __shared__ __attribute__((aligned(16))) char smem[kP9Lds];  // ONE LDS object (glds waits)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / G::WN, wc = wave % G::WN;
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    int b = blockIdx.x;
+    if (a.xcd_swizzle) {
+        const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = b % 8;
+        b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+    }
+    const int mt = b % ntt, vt = b / ntt;
+    const int m0 = mt * G::BM, n0 = vt * G::BN;
+    float2* cmb = reinterpret_cast<float2*>(smem + 4 * kP9Slot);
+    const int* lab = reinterpret_cast<const int*>(smem + kP9LabOff);
+    // labels (low dwords) by LDS DMA first: an ordinary load would make hipcc drain the queue
+    if (wave < 4) {
+        const int64_t* src = a.labels + int64_t(min(m0 + wave * 64 + lane, a.N - 1)) * a.lb;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + kP9LabOff + wave * 256),
+                                         4, 0, 0);
+    }
+    f32x4_t acc[G::kMR][G::kNR];
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int nk = a.H / kP9BK;  // even, >= 2
+    p9_issue(a, smem, m0, n0, 0, wave, lane);
+    p9_issue(a, smem, m0, n0, 1, wave, lane);
+    if (nk > 2) {
+        p9_issue(a, smem, m0, n0, 2, wave, lane);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // labels + K-step 0 landed
+    } else {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    pp_barrier();
+    if (wr == 1) pp_barrier();
+    bf16x8_t af[8], bfr[4];
+    const int fr = lane & 15, fc = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        const char* At = smem + (kt & 3) * kP9Slot;
+        const char* Bt = At + G::BM * 64;
+        if (!(a.dbg & 4)) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = lds_frag64(Bt, wc * 64 + j * 16 + fr, fc);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) af[i] = lds_frag64(At, wr * 128 + i * 16 + fr, fc);
+        }
+        if (kt + 3 < nk) {
+            if (!(a.dbg & 2)) p9_issue(a, smem, m0, n0, kt + 3, wave, lane);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K-step kt+1 landed
+        } else if (kt + 2 < nk) {
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads retired: the slot may be restaged
+        pp_barrier();
+        __builtin_amdgcn_s_setprio(1);
+        if (!(a.dbg & 1)) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+    }
+    if (wr == 0) pp_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rt = wr * G::kWRows + i * 16 + (lane >> 4) * 4 + q;
+            float x[G::kNR];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) {
+                const int v = n0 + wc * G::kWCols + j * 16 + cl;
+                x[j] = v < a.V ? acc[i][j][q] : -INFINITY;
+                mx = fmaxf(mx, x[j]);
+            }
+            mx = row16_max(mx);
+            const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) sm += exp2_fast(fmaf(x[j], kLog2e, ml2e));
+            sm = row16_sum(sm);
+            if (cl == 0) cmb[wc * G::BM + rt] = make_float2(mx, sm);
+            const int dy = lab[rt] - (n0 + wc * G::kWCols);
+            if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+                float xy = x[0];
+#pragma unroll
+                for (int j = 1; j < G::kNR; ++j) xy = (dy >> 4) == j ? x[j] : xy;
+                a.xlab[m0 + rt] = xy;
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        if (m0 + t >= a.N) continue;
+        float m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < G::WN; ++c) m = fmaxf(m, cmb[c * G::BM + t].x);
+        float sm = 0.f;
+        if (m != -INFINITY) {
+#pragma unroll
+            for (int c = 0; c < G::WN; ++c) {
+                const float2 p = cmb[c * G::BM + t];
+                sm += p.x == -INFINITY ? 0.f : p.y * exp2_fast((p.x - m) * kLog2e);
+            }
+        }
+        a.part[int64_t(m0 + t) * a.nvt + vt] = make_float2(m, sm);
+    }
+}
+
 // ------------------------------------------------------------------ persistent ping-pong
 // k_lmhead_pingpong's schedule as ONE stream over all of a workgroup's tiles (tile j of
 // workgroup b is b + j·gridDim): the half-tile stream, its slots (parity of the GLOBAL
@@ -1107,7 +1260,7 @@ void lm_set_dbg(int v) { g_lm_dbg = v; }
 }  // namespace trlx
 
 extern "C" int trlx_lmhead_set_variant(int v) {
-    TRLX_REQUIRE(v >= 0 && v <= 8, TRLX_ERR_ARG, "lmhead variant 0..8");
+    TRLX_REQUIRE(v >= 0 && v <= 9, TRLX_ERR_ARG, "lmhead variant 0..9");
     g_lm_variant = v;
     return TRLX_OK;
 }
@@ -1162,6 +1315,13 @@ static int lm_launch_pp2(const LmHeadArgs& a, hipStream_t stream) {
     return check_launch("k_lmhead_pp2");
 }
 
+static int lm_launch_pp9(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntt = (a.N + LmBig::BM - 1) / LmBig::BM;
+    TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    hipLaunchKernelGGL(k_lmhead_pp9, dim3(unsigned(ntt * a.nvt)), dim3(512), 0, stream, a);
+    return check_launch("k_lmhead_pp9");
+}
+
 static int lm_launch_pingpong(const LmHeadArgs& a, hipStream_t stream) {
     const int64_t ntt = (a.N + LmBig::BM - 1) / LmBig::BM;
     TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
@@ -1200,7 +1360,8 @@ extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void*
     const int var = lm_variant(N, H);
     a.xcd_swizzle = var == 4 || var == 6;
     a.dbg = g_lm_dbg;
-    int rc = var == 8              ? lm_launch_pp2(a, (hipStream_t)stream)
+    int rc = var == 9              ? lm_launch_pp9(a, (hipStream_t)stream)
+             : var == 8            ? lm_launch_pp2(a, (hipStream_t)stream)
              : var == 7            ? lm_launch_pp_persist(a, (hipStream_t)stream)
              : var == 5 || var == 6 ? lm_launch_pingpong(a, (hipStream_t)stream)
              : var == 1            ? lm_launch_persist<LmBig>(a, (hipStream_t)stream)
