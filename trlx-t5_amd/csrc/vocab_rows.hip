@@ -41,6 +41,7 @@ struct RowArgs {
     const double* stats;
     int unbiased;
     int order;                // vector order of the resident rows (0 step-major, 1 wave-major)
+    int spol;                 // gradient-row store cache policy (tuning "store_policy", see g_store_pol)
     const int64_t* mask;
     const double* msum;
     double msum_host;
@@ -243,7 +244,15 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
                 for (int e = 0; e < EPV; ++e)
                     if (e == ey) f[e] = gy;
             }
-            __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, launder_int(voff) + k * vstep * 16, 0, kAuxNT);
+            const vec4u pk = DT::pack(f);
+            const int off = launder_int(voff) + k * vstep * 16;
+            switch (a.spol) {  // wave-uniform; cache policy of the gradient stream
+                case 1: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 0); break;
+                case 2: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 16); break;
+                case 3: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 17); break;
+                case 4: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 18); break;
+                default: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, kAuxNT); break;
+            }
         }
     } else {
 #pragma unroll
@@ -412,6 +421,7 @@ static int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 6 wave
 static int g_stream_threads = 0;
 static int g_stream_unroll = 0;
 static int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
+static int g_store_pol = 0;         // gradient-row stores: 0 nt (default), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
 // workgroup size.  Default: 512-thread workgroups (8 waves) -- measured on MI355X (C2,
@@ -450,6 +460,7 @@ template <int MODE, class DT>
 static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     RowArgs a = a0;
     a.order = g_row_order;
+    a.spol = g_store_pol;
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
@@ -729,6 +740,9 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
         g_stream_threads = int(value);
     } else if (k == "lmhead_dbg") {
         lm_set_dbg(int(value));
+    } else if (k == "store_policy") {
+        TRLX_REQUIRE(value >= 0 && value <= 4, TRLX_ERR_ARG, "store_policy: 0..4");
+        g_store_pol = int(value);
     } else if (k == "row_order") {
         TRLX_REQUIRE(value == 0 || value == 1, TRLX_ERR_ARG, "row_order: 0 or 1");
         g_row_order = int(value);
