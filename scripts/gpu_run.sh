@@ -26,17 +26,29 @@ for step in "$@"; do
         sweep_c4) B=128 T=128 V=32128 run sweep_c4 300 python tools/row_sweep.py ;;
         sweep_f32) DT=f32 run sweep_f32 300 python tools/row_sweep.py ;;
         bench) run bench 400 python bench.py ;;
-        bench_c3) run bench_c3 300 python bench.py --config c3 --cpu-seconds 0 ;;
+        bench_c3) run bench_c3 300 python bench.py --config c3 --cpu-seconds 10 ;;
         bench_c5) run bench_c5 300 python bench.py --config c5 --cpu-seconds 10 ;;
         profile_c5) run profile_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 \
-                     -o run -- python bench.py --steps 10 --warmup 3 --config c5 --cpu-seconds 0 --no-timers ;;
+                     -o run -- python bench.py --config c5 --cpu-seconds 0 ;;
         ilql) run ilql_tests 300 python -u -m pytest tests/test_gpu_ilql.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-        bench_c4) run bench_c4 300 python bench.py --config c4 --cpu-seconds 0 ;;
+        bench_c4) run bench_c4 300 python bench.py --config c4 --cpu-seconds 10 ;;
         profile_nt) run profile_nt 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_nt \
                      -o run -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-timers ;;
         bench_nt) run bench_nt 300 python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-timers ;;
         profile) run profile 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof \
-                     -o run -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 ;;
+                     -o run -- python bench.py --cpu-seconds 0 ;;
+        profile_c4) run profile_c4 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 \
+                     -o run -- python bench.py --config c4 --cpu-seconds 0 ;;
+        profile_c3) run profile_c3 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 \
+                     -o run -- python bench.py --config c3 --cpu-seconds 0 ;;
+        pmc_fetch_c4) run pmc_fetch_c4 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_c4 \
+                     -o run -- python bench.py --steps 5 --warmup 2 --config c4 --cpu-seconds 0 --no-timers ;;
+        pmc_write_c4) run pmc_write_c4 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_c4 \
+                     -o run -- python bench.py --steps 5 --warmup 2 --config c4 --cpu-seconds 0 --no-timers ;;
+        pmc_fetch_c3) run pmc_fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_c3 \
+                     -o run -- python bench.py --steps 5 --warmup 2 --config c3 --cpu-seconds 0 --no-timers ;;
+        pmc_write_c3) run pmc_write_c3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_c3 \
+                     -o run -- python bench.py --steps 5 --warmup 2 --config c3 --cpu-seconds 0 --no-timers ;;
         pmc_fetch_c5) run pmc_fetch_c5 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_c5 \
                      -o run -- python bench.py --steps 3 --warmup 1 --config c5 --cpu-seconds 0 --no-timers ;;
         pmc_write_c5) run pmc_write_c5 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_c5 \
