@@ -100,3 +100,38 @@ def test_lmhead_every_variant_vs_oracle(variant):
                                        msg=f"variant {variant} N={N} H={H} V={V}")
     finally:
         _lib.call("trlx_lmhead_set_variant", 0)
+
+
+def test_experience_from_hidden_vs_oracle():
+    """PPOHotPath.experience_from_hidden (lm_head folded into the experience step) against the
+    oracle experience on fp64 logits = h·Wᵀ: lp / ref_lp / rewards / returns, then the loss
+    side runs on top (the GAE moments feed it as in the logits path)."""
+    B, T, H, V = 6, 11, 192, 1531
+    g = torch.Generator().manual_seed(21)
+    h = (torch.randn(B, T, H, generator=g) * 0.3).to(torch.bfloat16)
+    hr = (h.float() + 0.05 * torch.randn(B, T, H, generator=g)).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * 0.3).to(torch.bfloat16)
+    wr = (w.float() + 0.02 * torch.randn(V, H, generator=g)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, T), generator=g)
+    old_values = torch.randn(B, T, generator=g)
+    values = old_values + 0.3 * torch.randn(B, T, generator=g)
+    scores = torch.randn(B, generator=g) * 5
+    cfg = P.PPOConfig()
+    hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    hp.experience_from_hidden(h.to(DEV), w.to(DEV), hr.to(DEV), wr.to(DEV), labels.to(DEV), old_values.to(DEV),
+                              scores.to(DEV))
+    torch.cuda.synchronize()
+    logits = (h.double() @ w.double().t())
+    ref_logits = (hr.double() @ wr.double().t())
+    lp = orc.logprobs_from_logits(logits, labels)
+    ref_lp = orc.logprobs_from_logits(ref_logits, labels)
+    torch.testing.assert_close(hp.lp_old.cpu().double(), lp, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(hp.ref_lp.cpu().double(), ref_lp, rtol=1e-5, atol=1e-4)
+    rewards = orc.kl_penalty_rewards(lp.float(), ref_lp.float(), 0.05, scores)
+    torch.testing.assert_close(hp.rewards.cpu(), rewards, rtol=1e-4, atol=1e-5)
+    adv, ret = orc.gae(old_values, rewards, T, 1.0, 0.95, use_whitening=False)
+    torch.testing.assert_close(hp.returns.cpu(), ret, rtol=1e-4, atol=1e-4)
+    new_logits = (logits + 0.01).to(torch.bfloat16).to(DEV)  # any policy logits for the loss side
+    loss, stats, dl, dv = hp.policy_loss(new_logits, labels.to(DEV), values.to(DEV), old_values.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all() and torch.isfinite(dl.float()).all()

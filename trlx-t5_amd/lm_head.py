@@ -4,8 +4,10 @@
       == logprobs_from_logits(hidden @ weight.T, labels)     (modeling.py:37-41 after the
          lm_head of ppo_models.py:640 / :274 / :588), experience side (no gradient)
 
-The [.., V] logits are never written to HBM: MFMA tiles of 128 tokens x 128 vocab keep them
-in registers and reduce each tile to a partial (max, Σexp) per token (csrc/lmhead_rows.hip).
+The [.., V] logits are never written to HBM: MFMA tiles of 256 tokens x 256 vocab (ping-pong
+schedule; 128 x 128 for small N) keep them in registers and reduce each tile to a partial
+(max, Σexp) per token (csrc/lmhead_rows.hip).  PPOHotPath.experience_from_hidden runs the
+experience step this way.
 """
 import torch
 

@@ -74,6 +74,7 @@ class PPOHotPath:
         nbytes = _lib.query("trlx_ppo_workspace_bytes", B, T)
         self.workspace = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)  # tickets re-armed in-kernel
         self.dlogits = None
+        self.lm_ws = None  # lm_head partials workspace (experience_from_hidden)
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
         self.timer_names = None  # optional subset of launch names to instrument (None = all)
 
@@ -116,6 +117,48 @@ class PPOHotPath:
                   logits.stride(0), logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1),
                   self.lp_old.data_ptr(), self.ref_lp.data_ptr(), _lib.F32, None, None, s.cuda_stream)
         self._ev_end("experience", s)
+        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
+        return self.lp_old, self.ref_lp
+
+    def experience_from_hidden(self, hidden, weight, ref_hidden, ref_weight, labels, old_values, scores,
+                               lengths=None, mask=None, group=None):
+        """K1 with the lm_head folded in: lp / ref_lp straight from the policy's
+        and the reference model's last hidden states ([B, T, H] bf16) and lm_head weights
+        ([V, H] bf16) — `logits = lm_head(h)` (ppo_models.py:640, :274, :588) followed by
+        logprobs_from_logits (ppo_orchestrator.py:154-155) without the [B, T, V] logits ever
+        reaching HBM (two MFMA launches, trlx_lmhead_logprobs) — then the same GAE tail."""
+        B, T, V = self.B, self.T, self.V
+        for h, w in ((hidden, weight), (ref_hidden, ref_weight)):
+            if h.dim() != 3 or tuple(h.shape[:2]) != (B, T) or w.dim() != 2 or w.shape[0] != V or \
+                    w.shape[1] != h.shape[2] or h.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+                raise ValueError(f"hidden {tuple(h.shape)}/{h.dtype} and weight {tuple(w.shape)}/{w.dtype} do not "
+                                 f"match the hot path ({B},{T},H) x ({V},H) bf16")
+        if not labels.is_contiguous():
+            raise ValueError("labels must be contiguous")
+        s = torch.cuda.current_stream(self.device)
+        self.distributed = dist.is_available() and dist.is_initialized()
+        g_mom, work = None, None
+        if self.ctl is not None:
+            g_mom, work = self.ctl._global_moments(scores, group, async_op=True)
+        N = B * T
+        nbytes = _lib.query("trlx_lmhead_workspace_bytes", N, V)
+        if self.lm_ws is None or self.lm_ws.numel() < nbytes:
+            self.lm_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self._ev("experience", s)
+        for h, w, out in ((hidden, weight, self.lp_old), (ref_hidden, ref_weight, self.ref_lp)):
+            H = h.shape[2]
+            if h.stride(2) != 1 or h.stride(1) % 8 or h.stride(0) != T * h.stride(1) or h.data_ptr() % 16:
+                h = h.contiguous()
+            if w.stride(1) != 1 or w.stride(0) % 8 or w.data_ptr() % 16:
+                w = w.contiguous()
+            _lib.call("trlx_lmhead_logprobs", h.data_ptr(), h.stride(1), w.data_ptr(), w.stride(0), N, H, V,
+                      labels.data_ptr(), 1, out.data_ptr(), _lib.F32, None, self.lm_ws.data_ptr(), s.cuda_stream)
+        self._ev_end("experience", s)
+        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
+        return self.lp_old, self.ref_lp
+
+    def _experience_tail(self, s, labels, old_values, scores, lengths, mask, group, g_mom, work):
+        B, T = self.B, self.T
         if work is not None:
             work.wait()
         if self.tail_done is not None:  # previous loss tail: reads adv_stats[3] + token records, updates beta
@@ -133,7 +176,6 @@ class PPOHotPath:
         self._ev_end("rollout_gae", s)
         if self.distributed:
             dist.all_reduce(self.adv_stats[:3], dist.ReduceOp.SUM, group=group)
-        return self.lp_old, self.ref_lp
 
     # -------------------------------------------------------------- K2
     def policy_loss(self, new_logits, labels, values, old_values, mask=None):
