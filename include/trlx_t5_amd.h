@@ -294,7 +294,7 @@ int64_t trlx_lmhead_workspace_bytes(int64_t N, int64_t V);
  * in flight; 2 256x256 tiles, 2 barriers per K-step; 3 128x128 tiles; 4 = 2 with an XCD-aware
  * tile order; 5 256x256 ping-pong (two wave groups staggered by a barrier), 4 phases per
  * K-step; 6 = 5 with the XCD-aware order; 7 persistent ping-pong; 8 ping-pong, 2 phases per
- * K-step; 9 ping-pong over a 4-slot ring of 32-deep K-steps).  Results identical up to fp32 summation order.  Set before sizing the workspace
+ * K-step; 9 ping-pong over a 4-slot ring of 32-deep K-steps; 10 persistent form of 8).  Results identical up to fp32 summation order.  Set before sizing the workspace
  * (the vocab tile width changes it). */
 int trlx_lmhead_set_variant(int variant);
 int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,

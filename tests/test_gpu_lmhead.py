@@ -84,7 +84,7 @@ def test_lmhead_c2_shape_rows_and_determinism():
     torch.testing.assert_close(lp1[rows.to(DEV)].cpu().double(), want, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_lmhead_every_variant_vs_oracle(variant):
     """Every tile kernel (1 persistent, 2/4 256x256 tiles, 3 128x128, 5/6 ping-pong 256x256, 7 persistent
     ping-pong)
@@ -93,7 +93,8 @@ def test_lmhead_every_variant_vs_oracle(variant):
     from trlx_t5_amd import _lib
     try:
         _lib.call("trlx_lmhead_set_variant", variant)
-        for N, H, V, sc in [(300, 64, 1000, 0.5), (513, 768, 2051, 0.1), (2053, 192, 300, 0.3), (260, 4096, 517, 0.03)]:
+        for N, H, V, sc in [(300, 64, 1000, 0.5), (513, 768, 2051, 0.1), (2053, 192, 300, 0.3), (260, 4096, 517, 0.03),
+                            (4096, 64, 4100, 0.5), (2304, 128, 7937, 0.3)]:  # > 256 tiles: 2 per persistent workgroup
             h, w, y = case(N, H, V, 17 * variant + N, sc)
             lp = P.lm_head_logprobs(h.to(DEV), w.to(DEV), y.to(DEV), out_dtype=torch.float32)
             torch.testing.assert_close(lp.cpu().double(), oracle_lp(h, w, y), rtol=1e-5, atol=1e-4,

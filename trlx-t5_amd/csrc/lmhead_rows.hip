@@ -1029,6 +1029,11 @@ __global__ __launch_bounds__(512) void k_lmhead_pp_persist(LmHeadArgs a, int nti
             m0 = xm0;
             n0 = xn0;
             jj = j + 1;
+            if (t_kt >= nk) {  // nk == 1: two K-steps ahead is tile j + 2
+                t_kt -= nk;
+                jj = j + 2;
+                tile_origin(jj, m0, n0);
+            }
         }
         if (t_kt == 0 && kind == 0) pp2_issue_labels(a, smem, m0, jj % kPPLabRing, wave, lane);
         pp2_issue(a, smem, m0, n0, t_kt, kind, (g + d) & 1, wave, lane);
@@ -1187,6 +1192,194 @@ __global__ __launch_bounds__(512) void k_lmhead_pp_persist(LmHeadArgs a, int nti
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------------ persistent 2-phase ping-pong
+// k_lmhead_pp2's schedule (2 phases of 32 MFMAs per 64-deep K-step) as ONE stream over all of
+// a workgroup's tiles, as k_lmhead_pp_persist does for the 4-phase form: the half-tile stream
+// (HA0/HB0/HB1 of K-step g+1 issued in phase A of step g, HA1(g+1) in phase B), its slots
+// (parity of the global K-step index) and the counted waits (vmcnt(6) / vmcnt(2)) run across
+// tile boundaries; labels arrive by LDS DMA just ahead of each tile's first half-tile; the
+// epilogue is per wave group (one extra barrier per tile); past the end the issues fetch
+// clamped rows of a phantom tile so the counts stay exact.
+__global__ __launch_bounds__(512) void k_lmhead_pp2_persist(LmHeadArgs a, int ntiles) {
+    typedef LmBig G;
+    __shared__ __attribute__((aligned(16))) char smem[kPP2Lds];  // ONE LDS object (glds waits)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / G::WN, wc = wave % G::WN;
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    const int nk = a.H / kLmBK;
+    const int mine = (ntiles - int(blockIdx.x) + int(gridDim.x) - 1) / int(gridDim.x);
+    if (mine <= 0) return;
+    float2* cmb = reinterpret_cast<float2*>(smem + kPPStageBytes);
+    const int* labs = reinterpret_cast<const int*>(smem + kPPLabOff);
+    auto tile_origin = [&](int j, int& m0, int& n0) {
+        const int t = int(blockIdx.x) + j * int(gridDim.x);
+        m0 = (t % ntt) * G::BM;
+        n0 = (t / ntt) * G::BN;
+    };
+    int cm0, cn0, xm0, xn0;  // tile j / tile j+1 origins
+    tile_origin(0, cm0, cn0);
+    tile_origin(1, xm0, xn0);
+    // kinds [k0, k1) of K-step kt+1 of tile j (global index g+1): the current tile or the next
+    auto issue_next = [&](int j, int kt, int g, int k0, int k1) __attribute__((always_inline)) {
+        int t_kt = kt + 1, m0 = cm0, n0 = cn0, jj = j;
+        if (t_kt >= nk) {
+            t_kt = 0;
+            m0 = xm0;
+            n0 = xn0;
+            jj = j + 1;
+        }
+        (void)jj;
+        for (int kind = k0; kind < k1; ++kind) pp2_issue(a, smem, m0, n0, t_kt, kind, (g + 1) & 1, wave, lane);
+    };
+
+    f32x4_t acc[G::kMR][G::kNR];
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // prologue: tile 0's labels and all of K-step 0; HA0/HB0/HB1 retired, HA1 may stay in flight
+    pp2_issue_labels(a, smem, cm0, 0, wave, lane);
+#pragma unroll
+    for (int kind = 0; kind < 4; ++kind) pp2_issue(a, smem, cm0, cn0, 0, kind, 0, wave, lane);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    pp_barrier();
+    if (wr == 1) pp_barrier();  // group 1 runs one barrier behind
+    bf16x8_t af[2][4];
+    bf16x8_t bfr[2][2][2];
+    const int fr = lane & 15, fc = lane >> 4;
+    for (int j = 0; j < mine; ++j) {
+        for (int kt = 0; kt < nk; ++kt) {
+            const int g = j * nk + kt;
+            const char* buf = smem + (g & 1) * 4 * kPPHalf;
+            // ---- phase A: rows qm = 0
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[ks][i] = lds_frag(buf, wr * 64 + i * 16 + fr, ks * 4 + fc);
+#pragma unroll
+            for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj)
+                        bfr[qn][ks][jj] = lds_frag(buf + (1 + qn) * kPPHalf, wc * 32 + jj * 16 + fr, ks * 4 + fc);
+            issue_next(j, kt, g, 0, 3);
+            if (kt == 0 && wave < 4) {  // tile j+1's labels, youngest op: counted exactly
+                pp2_issue_labels(a, smem, xm0, (j + 1) % kPPLabRing, wave, lane);
+                asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // HA1(g) landed
+            } else {
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // HA1(g) landed
+            }
+            pp_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj)
+                            acc[i][qn * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                af[ks][i], bfr[qn][ks][jj], acc[i][qn * 2 + jj], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            pp_barrier();
+            // ---- phase B: rows qm = 1
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    af[ks][i] = lds_frag(buf + 3 * kPPHalf, wr * 64 + i * 16 + fr, ks * 4 + fc);
+            issue_next(j, kt, g, 3, 4);
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // K-step g+1's HA0/HB0/HB1 landed
+            pp_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int qn = 1; qn >= 0; --qn)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj)
+                            acc[4 + i][qn * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                af[ks][i], bfr[qn][ks][jj], acc[4 + i][qn * 2 + jj], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            pp_barrier();
+        }
+        // ---- tile epilogue, per wave group (k_lmhead_pp_persist's)
+        const int m0 = cm0, n0 = cn0;
+        const int vt = n0 / G::BN;
+        const int* lab = labs + (j % kPPLabRing) * G::BM;
+        const int cl = launder_int(lane & 15);
+        const int rbase = launder_int(wr * G::kWRows + (lane >> 4) * 4);
+        float2* cmbw = cmb + launder_int(wc * G::BM);
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i) {
+            const i32x4_t lab4 = lds_load_i4(lab + rbase + i * 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rt = rbase + i * 16 + q;
+                float x[G::kNR];
+                float mx = -INFINITY;
+#pragma unroll
+                for (int jj = 0; jj < G::kNR; ++jj) {
+                    const int v = n0 + wc * G::kWCols + jj * 16 + cl;
+                    x[jj] = v < a.V ? acc[i][jj][q] : -INFINITY;
+                    mx = fmaxf(mx, x[jj]);
+                }
+                mx = row16_max(mx);
+                const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
+                float sm = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < G::kNR; ++jj) sm += exp2_fast(fmaf(x[jj], kLog2e, ml2e));
+                sm = row16_sum(sm);
+                if (cl == 0) lds_store_f2(cmbw + rt, mx, sm);
+                const int dy = lab4[q] - (n0 + wc * G::kWCols);
+                if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+                    float xy = x[0];
+#pragma unroll
+                    for (int jj = 1; jj < G::kNR; ++jj) xy = (dy >> 4) == jj ? x[jj] : xy;
+                    a.xlab[m0 + rt] = xy;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+            for (int jj = 0; jj < G::kNR; ++jj) acc[i][jj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();  // the group's four waves published their partials
+        {
+            const int gt = tid - wr * 256;
+            if (gt < 128 && m0 + wr * 128 + gt < a.N) {
+                const int r = wr * 128 + gt;
+                float2 pw[G::WN];
+                float m = -INFINITY;
+#pragma unroll
+                for (int c2 = 0; c2 < G::WN; ++c2) {
+                    pw[c2] = lds_load_f2(cmb + c2 * G::BM + r);
+                    m = fmaxf(m, pw[c2].x);
+                }
+                float sm = 0.f;
+                if (m != -INFINITY) {
+#pragma unroll
+                    for (int c2 = 0; c2 < G::WN; ++c2)
+                        sm += pw[c2].x == -INFINITY ? 0.f : pw[c2].y * exp2_fast((pw[c2].x - m) * kLog2e);
+                }
+                a.part[int64_t(m0 + r) * a.nvt + vt] = make_float2(m, sm);
+            }
+        }
+        cm0 = xm0;
+        cn0 = xn0;
+        tile_origin(j + 2, xm0, xn0);
+    }
+    if (wr == 0) pp_barrier();  // balance group 1's extra barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // One wave per token: merge the nvt partials (fixed order per lane, then a fixed butterfly).
 __global__ __launch_bounds__(256) void k_lmhead_combine(LmHeadArgs a, void* lp, int lp_dtype, float* lse_out) {
     const int lane = threadIdx.x & 63;
@@ -1260,7 +1453,7 @@ void lm_set_dbg(int v) { g_lm_dbg = v; }
 }  // namespace trlx
 
 extern "C" int trlx_lmhead_set_variant(int v) {
-    TRLX_REQUIRE(v >= 0 && v <= 9, TRLX_ERR_ARG, "lmhead variant 0..9");
+    TRLX_REQUIRE(v >= 0 && v <= 10, TRLX_ERR_ARG, "lmhead variant 0..10");
     g_lm_variant = v;
     return TRLX_OK;
 }
@@ -1315,6 +1508,14 @@ static int lm_launch_pp2(const LmHeadArgs& a, hipStream_t stream) {
     return check_launch("k_lmhead_pp2");
 }
 
+static int lm_launch_pp2_persist(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntiles = int64_t((a.N + LmBig::BM - 1) / LmBig::BM) * a.nvt;
+    TRLX_REQUIRE(ntiles < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    const int grid = int(ntiles < lm_num_cus() ? ntiles : lm_num_cus());
+    hipLaunchKernelGGL(k_lmhead_pp2_persist, dim3(grid), dim3(512), 0, stream, a, int(ntiles));
+    return check_launch("k_lmhead_pp2_persist");
+}
+
 static int lm_launch_pp9(const LmHeadArgs& a, hipStream_t stream) {
     const int64_t ntt = (a.N + LmBig::BM - 1) / LmBig::BM;
     TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
@@ -1360,7 +1561,8 @@ extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void*
     const int var = lm_variant(N, H);
     a.xcd_swizzle = var == 4 || var == 6;
     a.dbg = g_lm_dbg;
-    int rc = var == 9              ? lm_launch_pp9(a, (hipStream_t)stream)
+    int rc = var == 10             ? lm_launch_pp2_persist(a, (hipStream_t)stream)
+             : var == 9            ? lm_launch_pp9(a, (hipStream_t)stream)
              : var == 8            ? lm_launch_pp2(a, (hipStream_t)stream)
              : var == 7            ? lm_launch_pp_persist(a, (hipStream_t)stream)
              : var == 5 || var == 6 ? lm_launch_pingpong(a, (hipStream_t)stream)
