@@ -213,3 +213,34 @@ def test_overlapped_loss_tail_matches_serial():
     for a, b in zip(outs[False], outs[True]):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+def test_hot_path_device_state_with_decoder_lengths():
+    """C3-style decoder-length masks with the device state: the transformed score lands on
+    column L_b - 1, padding stays zero, the loss normalisers use the mask."""
+    B, Tn, V = 10, 21, 777
+    g = torch.Generator().manual_seed(13)
+    logits, ref_logits, new_logits, labels, old_values, values = _step_inputs(B, Tn, V, 77)
+    L = torch.randint(1, Tn + 1, (B,), generator=g)
+    L[0] = Tn
+    mask = (torch.arange(Tn)[None, :] < L[:, None]).long()
+    old_values = old_values.masked_fill(mask == 0, 0)
+    cfg = P.PPOConfig(scale_reward="running", cliprange_reward=3)
+    c = P.PPOControlState.from_config(cfg, DEV, n_steps=B)
+    hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.0, ctl=c)
+    oc = orc.ScoreControl("running", 3)
+    okl = orc.AdaptiveKLController(0.05, 6, 10000)
+    for step in range(2):
+        scores = torch.randn(B, generator=g) * 8
+        beta = okl.value
+        loss, stats, _, _ = hp.step(cuda(logits), cuda(ref_logits), cuda(new_logits), cuda(labels), cuda(old_values),
+                                    cuda(values), cuda(scores), lengths=cuda(L), mask=cuda(mask))
+        torch.cuda.synchronize()
+        s_t, _, _ = oc(scores)
+        ref = orc.ppo_step_reference(logits.float(), ref_logits.float(), new_logits.float(), labels, old_values,
+                                     values, s_t, kl_coef=beta, lengths=L, mask=mask)
+        torch.testing.assert_close(hp.rewards.cpu(), ref["rewards"], **RT32)
+        assert torch.all(hp.rewards.cpu()[mask == 0] == 0)
+        torch.testing.assert_close(loss.cpu().reshape(()), ref["loss"], rtol=1e-5, atol=1e-6)
+        okl.update(float(stats[8]), n_steps=B)
+        assert c.host()["kl_coef"] == okl.value
