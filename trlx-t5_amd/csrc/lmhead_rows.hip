@@ -650,11 +650,7 @@ __global__ __launch_bounds__(512) void k_lmhead_pp2(LmHeadArgs a) {
     const int mt = b % ntt, vt = b / ntt;
     const int m0 = mt * G::BM, n0 = vt * G::BN;
     float2* cmb = reinterpret_cast<float2*>(smem + kPPStageBytes);
-    int* lab = reinterpret_cast<int*>(smem + kPPStageBytes + G::WN * G::BM * 8);
-    for (int t = tid; t < G::BM; t += G::kThreads) {
-        const int m = m0 + t;
-        lab[t] = m < a.N ? int(a.labels[int64_t(m) * a.lb]) : -1;
-    }
+    const int* lab = reinterpret_cast<const int*>(smem + kPPStageBytes + G::WN * G::BM * 8);
     f32x4_t acc[G::kMR][G::kNR];
 #pragma unroll
     for (int i = 0; i < G::kMR; ++i)
@@ -664,7 +660,15 @@ __global__ __launch_bounds__(512) void k_lmhead_pp2(LmHeadArgs a) {
     // K-step 0: all four half-tiles; wait for HA0/HB0/HB1 (HA1 may stay in flight)
 #pragma unroll
     for (int kind = 0; kind < 4; ++kind) pp_issue(a, smem, m0, n0, kind, wave, lane);
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // labels (low dwords) by LDS DMA behind the operands: no ordinary load (hipcc would wait
+    // for it before the first DMA), no latency ahead of K-step 0; read in the epilogue only
+    if (wave < 4) {
+        const int64_t* src = a.labels + int64_t(min(m0 + wave * 64 + lane, a.N - 1)) * a.lb;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(smem + kPPStageBytes +
+                                                                                        G::WN * G::BM * 8 + wave * 256),
+                                         4, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // HA0/HB0/HB1 of K-step 0 (HA1 + labels may fly)
     pp_barrier();
     if (wr == 1) pp_barrier();
     if ((a.dbg & 8) && wr == 1) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
