@@ -282,7 +282,12 @@ def ilql_sample_step(logits, target_qs, vs, beta=1.0, top_k=20, temperature=1.0,
     if logit_mask is not None:
         if input_ids is None:
             raise ValueError("logit_mask needs input_ids")
-        mask = logit_mask.to(device=dev, dtype=torch.uint8).contiguous()
+        mask = logit_mask.to(device=dev)
+        # bool and uint8 share the 1-byte layout: reinterpret instead of converting ([V', V]
+        # masks can be vocab x vocab — a per-step conversion would copy the whole table)
+        mask = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)
+        if mask.stride(-1) != 1:
+            mask = mask.contiguous()
         prev = input_ids[:, -1].to(device=dev, dtype=torch.int64).contiguous()
     q1 = rows[2] if len(rows) > 2 else None
     _lib.call("trlx_ilql_sample", rows[0].data_ptr(), rows[0].stride(0), rows[1].data_ptr(), rows[1].stride(0),
