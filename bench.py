@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--host-state", action="store_true",
                    help="PPO: keep beta as a host constant and skip the score RunningMoments/clip and the KL "
                         "controller update (the default runs them on device, ppo_config.yml settings)")
+    p.add_argument("--logits-dtype", default="bf16", choices=("bf16", "fp32"),
+                   help="PPO logits dtype (bf16: the T5/UL2 path and BASELINE's C2 row; fp32: the reference's GPT "
+                        "path)")
     p.add_argument("--no-overlap", action="store_true",
                    help="PPO: run the loss tail on the main stream (default: side stream, beside the next step's "
                         "experience rows)")
@@ -142,9 +145,9 @@ def _cores():
     return max(1, min(cores, 16))
 
 
-def make_inputs(torch, B, T, V, dev, seed, masked):
+def make_inputs(torch, B, T, V, dev, seed, masked, dtype=None):
     g = torch.Generator(device=dev).manual_seed(seed)
-    bf = torch.bfloat16
+    bf = dtype or torch.bfloat16
     logits = torch.randn(B, T, V, generator=g, device=dev, dtype=torch.float32).to(bf)
     ref_logits = (logits.float() + 0.1 * torch.randn(B, T, V, generator=g, device=dev)).to(bf)
     new_logits = (logits.float() + 0.05 * torch.randn(B, T, V, generator=g, device=dev)).to(bf)
@@ -162,14 +165,15 @@ def make_inputs(torch, B, T, V, dev, seed, masked):
                 old_values=old_values, values=values, scores=scores, lengths=lengths, mask=mask)
 
 
-def cpu_baseline(torch, T, V, seconds):
-    """Oracle (reference PyTorch ops, native bf16 like the T5/UL2 path) on host cores."""
+def cpu_baseline(torch, T, V, seconds, dtype=None):
+    """Oracle (reference PyTorch ops, in the logits dtype: native bf16 like the T5/UL2 path, or
+    fp32 like the GPT path) on host cores."""
     from oracle import ppo_oracle as orc
     cores = _cores()
     torch.set_num_threads(cores)
     Bs = 8
     g = torch.Generator().manual_seed(123)
-    bf = torch.bfloat16
+    bf = dtype or torch.bfloat16
     logits = torch.randn(Bs, T, V, generator=g).to(bf)
     ref_logits = (logits.float() + 0.1 * torch.randn(Bs, T, V, generator=g)).to(bf)
     new_logits = (logits.float() + 0.05 * torch.randn(Bs, T, V, generator=g)).to(bf)
@@ -190,7 +194,7 @@ def cpu_baseline(torch, T, V, seconds):
         if el >= seconds:
             break
     return {"value": toks / el, "unit": "tokens/s", "cores": cores, "kind": "port",
-            "sample": f"{toks // (Bs * T)} steps of {Bs}x{T}x{V} bf16 (oracle ScoreControl + ppo_step_reference + "
+            "sample": f"{toks // (Bs * T)} steps of {Bs}x{T}x{V} {str(bf).replace('torch.', '')} (oracle ScoreControl + ppo_step_reference + "
                       f"AdaptiveKLController: reference ops incl. autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
 
 
@@ -216,6 +220,8 @@ def main():
             dist.init_process_group("gloo")
 
     B, T, V, desc = CONFIGS[args.config]
+    if args.logits_dtype == "fp32" and args.config != "c5":
+        desc = desc.replace("bf16 logits", "fp32 logits") + ("" if "logits" in desc else ", fp32 logits")
     ilql = args.config == "c5"
     masked = args.config == "c3"
     if ilql:
@@ -225,10 +231,11 @@ def main():
         def step():
             return hp.step(lg, qs, tqs, vs, batch)
     else:
-        x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked)
+        ldt = torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16
+        x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
         cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
         ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
-        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap)
+        hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap)
 
         def step():
             return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],
@@ -273,7 +280,7 @@ def main():
         doms = ("rows",)
     else:
         tokens = B * T
-        ab = algorithmic_bytes(V, 2, masked)
+        ab = algorithmic_bytes(V, 4 if args.logits_dtype == "fp32" else 2, masked)
         doms = ("experience", "loss")
     roof = None
     if kern_ms:
@@ -284,7 +291,7 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 rec = json.load(f)
-            traffic = rec.get(args.config, {}).get(dom)
+            traffic = rec.get(args.config + ("_fp32" if args.logits_dtype == "fp32" and not ilql else ""), {}).get(dom)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
                 "bytes_per_launch": int(round(ab[dom] * tokens)), "avg_launch_us": round(kern_ms[dom] * 1e3, 2),
@@ -295,7 +302,11 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_seconds > 0:
-            cpu = (ilql_cpu_baseline if ilql else cpu_baseline)(torch, T, V, args.cpu_seconds)
+            if ilql:
+                cpu = ilql_cpu_baseline(torch, T, V, args.cpu_seconds)
+            else:
+                cpu = cpu_baseline(torch, T, V, args.cpu_seconds,
+                                   torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16)
         ms = elapsed / args.steps * 1e3
         out = {
             "metric": METRIC_ILQL if ilql else METRIC,
@@ -311,7 +322,7 @@ def main():
             "dtype": "f32",  # arithmetic type; logits_dtype in config
             "data": "synthetic",
             "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world, "seq_len": T, "vocab": V,
-                       "logits_dtype": "fp32" if ilql else "bf16", "tokens_per_gpu_step": tokens,
+                       "logits_dtype": "fp32" if ilql else args.logits_dtype, "tokens_per_gpu_step": tokens,
                        "parallelism": f"dp{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -401,3 +401,27 @@ def test_fused_experience_tail_chunking(T):
         torch.testing.assert_close(torch.tensor(mu), (ref["returns"] - (old_values if L is None else
                                    old_values.masked_fill(mask == 0, 0))).mean().double().float(),
                                    rtol=1e-4, atol=1e-5)
+
+
+def test_hot_path_step_fp32_logits():
+    """The GPT path's fp32 logits (the reference's GPT heads are fp32) through the fused step."""
+    B, Tn, V = 8, 48, 50257
+    g = torch.Generator().manual_seed(31)
+    logits = torch.randn(B, Tn, V, generator=g)
+    ref_logits = logits + 0.1 * torch.randn(B, Tn, V, generator=g)
+    new_logits = logits + 0.05 * torch.randn(B, Tn, V, generator=g)
+    labels = torch.randint(0, V, (B, Tn), generator=g)
+    old_values = torch.randn(B, Tn, generator=g)
+    values = old_values + 0.3 * torch.randn(B, Tn, generator=g)
+    scores = torch.rand(B, generator=g) * 24 - 12
+    hp = P.PPOHotPath(P.PPOConfig(), B, Tn, V, torch.float32, DEV, kl_coef=0.05)
+    loss, stats, dlogits, dvalues = hp.step(cuda(logits), cuda(ref_logits), cuda(new_logits), cuda(labels),
+                                            cuda(old_values), cuda(values), cuda(scores))
+    torch.cuda.synchronize()
+    ref = orc.ppo_step_reference(logits, ref_logits, new_logits, labels, old_values, values, scores, kl_coef=0.05)
+    torch.testing.assert_close(hp.lp_old.cpu(), ref["lp"], **RT32)
+    torch.testing.assert_close(hp.rewards.cpu(), ref["rewards"], **RT32)
+    torch.testing.assert_close(loss.cpu().reshape(()), ref["loss"], rtol=1e-5, atol=1e-6)
+    assert dlogits.dtype == torch.float32
+    torch.testing.assert_close(dlogits.cpu(), ref["dlogits"], rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(dvalues.cpu(), ref["dvalues"], rtol=1e-5, atol=1e-9)

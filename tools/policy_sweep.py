@@ -20,9 +20,10 @@ def main():
     vals = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "0,1,2,3,4").split(",")]
     B, T, V, _ = bench.CONFIGS[cfg]
     dev = torch.device("cuda:0")
-    x = bench.make_inputs(torch, B, T, V, dev, seed=1, masked=cfg == "c3")
+    dt = torch.float32 if os.environ.get("DT") == "fp32" else torch.bfloat16
+    x = bench.make_inputs(torch, B, T, V, dev, seed=1, masked=cfg == "c3", dtype=dt)
     pc = P.PPOConfig()
-    hp = P.PPOHotPath(pc, B, T, V, torch.bfloat16, dev, kl_coef=0.05,
+    hp = P.PPOHotPath(pc, B, T, V, dt, dev, kl_coef=0.05,
                       ctl=P.PPOControlState.from_config(pc, dev, n_steps=B), overlap_tail=True)
 
     def step():
