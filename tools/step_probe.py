@@ -22,8 +22,9 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
     B, T, V, _ = bench.CONFIGS[cfg]
     dev = torch.device("cuda:0")
-    x = bench.make_inputs(torch, B, T, V, dev, seed=1, masked=cfg == "c3")
-    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05)
+    dt = torch.float32 if os.environ.get("DT") == "fp32" else torch.bfloat16
+    x = bench.make_inputs(torch, B, T, V, dev, seed=1, masked=cfg == "c3", dtype=dt)
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, dt, dev, kl_coef=0.05)
 
     def step():
         hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"], x["values"],

@@ -134,8 +134,12 @@ __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, cons
 // host checks strides and base phases; grad_buffer_like guarantees it), so dlogits are
 // written with the same aligned 16-B vectors.  The other instantiation writes elements.
 // LB512: launched with <= 512 threads, compiled for 6 waves per SIMD (opt-in knob).
-template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512>
-__global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vocab_rows(RowArgs a) {
+// NL > 0 (split residency, long fp32 rows): the row's last NL vector steps are DMA'd into
+// LDS (32 KB per workgroup at NL = 4) instead of VGPRs, so a 512-thread workgroup fits in
+// 128 VGPRs and two rows stay in flight per CU (a 201-KB fp32 row held whole in VGPRs
+// needs 1024 threads at ~88 VGPRs: one row per CU, its load / reduce / store phases exposed).
+template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0>
+__global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL ? 4 : 1)) void k_vocab_rows(RowArgs a) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     typedef typename DT::elem_t E;
@@ -169,6 +173,18 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
 #pragma unroll
     for (int k = 0; k < NV; ++k)
         v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, launder_int(voff) + k * vstep * 16, 0, kAuxNT);
+    __shared__ __attribute__((aligned(16))) vec4u lds_row[NL > 0 ? NL * 512 : 1];
+    if constexpr (NL > 0) {  // vector steps NV .. NV+NL-1 -> lds_row[kk][tid] (lane-linear per wave)
+        const char* body = reinterpret_cast<const char*>(r.x + r.s.head);
+        char* lbase = reinterpret_cast<char*>(lds_row) + (tid >> 6) * 1024;
+#pragma unroll
+        for (int kk = 0; kk < NL; ++kk) {
+            const int i = vbase + (NV + kk) * vstep;
+            const int ic = unsigned(i) < unsigned(nvec) ? i : 0;  // out-of-row lanes: any valid address
+            __builtin_amdgcn_global_load_lds(body + int64_t(ic) * 16,
+                                             (__attribute__((address_space(3))) void*)(lbase + kk * 8192), 16, 0, 0);
+        }
+    }
     const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
     const int64_t je = r.edge_index();
     const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
@@ -187,6 +203,18 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
             for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
             m = (unsigned(vbase + k * vstep) < unsigned(nvec)) ? fmaxf(m, mk) : m;
         }
+        if constexpr (NL > 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's DMAs (it reads only its own)
+#pragma unroll
+            for (int kk = 0; kk < NL; ++kk) {
+                float f[EPV];
+                DT::unpack(lds_row[kk * 512 + tid], f);
+                float mk = f[0];
+#pragma unroll
+                for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
+                m = (unsigned(vbase + (NV + kk) * vstep) < unsigned(nvec)) ? fmaxf(m, mk) : m;
+            }
+        }
         m = block_max(m, sh_max);
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
@@ -201,6 +229,17 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
             for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
             sum += (unsigned(vbase + k * vstep) < unsigned(nvec)) ? sk : 0.0f;
         }
+        if constexpr (NL > 0) {
+#pragma unroll
+            for (int kk = 0; kk < NL; ++kk) {
+                float f[EPV];
+                DT::unpack(lds_row[kk * 512 + tid], f);
+                float sk = 0.0f;
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
+                sum += (unsigned(vbase + (NV + kk) * vstep) < unsigned(nvec)) ? sk : 0.0f;
+            }
+        }
         sum = block_sum(sum, sh_sum);
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
@@ -211,6 +250,9 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
         return;
     }
 
+    if constexpr (NL > 0) {
+        if (MODE == kBwd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no reduction pass waited
+    }
     // (both reductions' barriers separate thread 0's s_ps writes from these reads)
     const PpoScalars ps = {s_ps[0], s_ps[1], s_ps[2], s_ps[3]};
     PolicyTerms pt = {1.f, 0.f, 0.f, false};
@@ -254,6 +296,24 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
                 default: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, kAuxNT); break;
             }
         }
+        if constexpr (NL > 0) {
+#pragma unroll
+            for (int kk = 0; kk < NL; ++kk) {
+                const int i = vbase + (NV + kk) * vstep;
+                float f[EPV];
+                DT::unpack(lds_row[kk * 512 + tid], f);
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+                if (i == iy) {
+                    const int ey = int(r.y - (r.s.head + int64_t(i) * EPV));
+#pragma unroll
+                    for (int e = 0; e < EPV; ++e)
+                        if (e == ey) f[e] = gy;
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, launder_int(voff) + (NV + kk) * vstep * 16, 0,
+                                                       kAuxNT);
+            }
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
@@ -265,6 +325,21 @@ __global__ __launch_bounds__(LB512 ? 512 : kMaxThreads, LB512 ? 6 : 1) void k_vo
                 for (int e = 0; e < EPV; ++e) {
                     const int64_t j = r.s.head + int64_t(i) * EPV + e;
                     DT::store1(drow, j, j == r.y ? gy : -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
+                }
+            }
+        }
+        if constexpr (NL > 0) {
+#pragma unroll
+            for (int kk = 0; kk < NL; ++kk) {
+                const int i = vbase + (NV + kk) * vstep;
+                if (unsigned(i) < unsigned(nvec)) {
+                    float f[EPV];
+                    DT::unpack(lds_row[kk * 512 + tid], f);
+#pragma unroll
+                    for (int e = 0; e < EPV; ++e) {
+                        const int64_t j = r.s.head + int64_t(i) * EPV + e;
+                        DT::store1(drow, j, j == r.y ? gy : -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
+                    }
                 }
             }
         }
@@ -422,6 +497,7 @@ static int g_stream_threads = 0;
 static int g_stream_unroll = 0;
 static int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
 static int g_store_pol = 0;         // gradient-row stores: 0 nt (default), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1
+static int g_split_lds = 0;         // long fp32 rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
 // workgroup size.  Default: 512-thread workgroups (8 waves) -- measured on MI355X (C2,
@@ -462,6 +538,18 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     a.order = g_row_order;
     a.spol = g_store_pol;
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
+    if constexpr (sizeof(typename DT::elem_t) == 4) {
+        // long fp32 rows: 21 vectors per thread in VGPRs + 4 in LDS, 512 threads, 2 rows per CU
+        const int64_t nvec = a.V / 4 + 1 + (kLineVecs - 1);
+        const bool want = g_split_lds == 2 || (g_split_lds == 0 && MODE != kFwd);
+        if (want && !g_row_variant && !g_resident_threads && nvec > 512 * 16 && nvec <= 512 * (21 + 4)) {
+            if (MODE == kFwd || rows_same_phase(a, 4))
+                hipLaunchKernelGGL((k_vocab_rows<DT, 21, MODE, true, false, 4>), grid, dim3(512), 0, stream, a);
+            else
+                hipLaunchKernelGGL((k_vocab_rows<DT, 21, MODE, false, false, 4>), grid, dim3(512), 0, stream, a);
+            return check_launch("k_vocab_rows (split LDS)");
+        }
+    }
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
     if (variant == 2 || g.nv == 0) {
@@ -740,6 +828,9 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
         g_stream_threads = int(value);
     } else if (k == "lmhead_dbg") {
         lm_set_dbg(int(value));
+    } else if (k == "split_lds") {
+        TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "split_lds: 0..2");
+        g_split_lds = int(value);
     } else if (k == "store_policy") {
         TRLX_REQUIRE(value >= 0 && value <= 4, TRLX_ERR_ARG, "store_policy: 0..4");
         g_store_pol = int(value);
