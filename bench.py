@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--no-overlap", action="store_true",
                    help="PPO: run the loss tail on the main stream (default: side stream, beside the next step's "
                         "experience rows)")
+    p.add_argument("--tune", action="append", default=[],
+                   help="key=value launch tuning (trlx_set_tuning; A/B only, results identical)")
     p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -205,6 +207,9 @@ def main():
     import __graft_entry__
     P = __graft_entry__.load_package()
     P.load_library()
+    for kv in args.tune:
+        k, v = kv.split("=")
+        P._lib.set_tuning(k, int(v))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -83,8 +83,10 @@ struct IlqlRowScalars {
     float inv_n;
 };
 
-template <class DT, int NV>
-__global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
+// NL > 0: split residency for long fp32 rows, as k_vocab_rows (vocab_rows.hip): the last NL
+// vector steps live in LDS (DMA), 512 threads, two rows in flight per CU.
+template <class DT, int NV, int NL = 0>
+__global__ __launch_bounds__(NL ? 512 : kMaxThreads, NL ? 4 : 1) void k_ilql_rows(trlx_ilql_args a) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     __shared__ float s_sc[4];
@@ -150,6 +152,18 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
 #pragma unroll
     for (int k = 0; k < NV; ++k)
         v[k] = __builtin_amdgcn_raw_buffer_load_b128(rin, launder_int(voff) + k * nthr * 16, 0, kAuxNT);
+    __shared__ __attribute__((aligned(16))) vec4u lds_row[NL > 0 ? NL * 512 : 1];
+    if constexpr (NL > 0) {  // vector steps NV .. NV+NL-1 -> lds_row[kk][tid]
+        const char* body = reinterpret_cast<const char*>(x + s.head);
+        char* lbase = reinterpret_cast<char*>(lds_row) + (tid >> 6) * 1024;
+#pragma unroll
+        for (int kk = 0; kk < NL; ++kk) {
+            const int i = tid - shift + (NV + kk) * nthr;
+            const int ic = unsigned(i) < unsigned(nvec) ? i : 0;
+            __builtin_amdgcn_global_load_lds(body + int64_t(ic) * 16,
+                                             (__attribute__((address_space(3))) void*)(lbase + kk * 8192), 16, 0, 0);
+        }
+    }
     const float xy = y_ok ? DT::load1(x, y) : NAN;
     int64_t je = -1;  // head element -> threads [0, head); tail element -> the last `tail` threads
     if (tid < s.head) je = tid;
@@ -166,6 +180,18 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
         for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
         m = (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? fmaxf(m, mk) : m;
     }
+    if constexpr (NL > 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's DMAs (it reads only its own)
+#pragma unroll
+        for (int kk = 0; kk < NL; ++kk) {
+            float f[EPV];
+            DT::unpack(lds_row[kk * 512 + tid], f);
+            float mk = f[0];
+#pragma unroll
+            for (int e = 1; e < EPV; ++e) mk = fmaxf(mk, f[e]);
+            m = (unsigned(tid - shift + (NV + kk) * nthr) < unsigned(nvec)) ? fmaxf(m, mk) : m;
+        }
+    }
     m = block_max(m, sh_max);
 #pragma unroll
     for (int k = 0; k < NV; ++k) launder(v[k]);
@@ -179,6 +205,17 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
 #pragma unroll
         for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
         sum += (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? sk : 0.0f;
+    }
+    if constexpr (NL > 0) {
+#pragma unroll
+        for (int kk = 0; kk < NL; ++kk) {
+            float f[EPV];
+            DT::unpack(lds_row[kk * 512 + tid], f);
+            float sk = 0.0f;
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
+            sum += (unsigned(tid - shift + (NV + kk) * nthr) < unsigned(nvec)) ? sk : 0.0f;
+        }
     }
     sum = block_sum(sum, sh_sum);
 #pragma unroll
@@ -212,6 +249,24 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_rows(trlx_ilql_args a) {
                 if (e == ey) f[e] = gy;
         }
         __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, launder_int(voff) + k * nthr * 16, 0, kAuxNT);
+    }
+    if constexpr (NL > 0) {
+#pragma unroll
+        for (int kk = 0; kk < NL; ++kk) {
+            const int i = tid - shift + (NV + kk) * nthr;
+            float f[EPV];
+            DT::unpack(lds_row[kk * 512 + tid], f);
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+            if (i == iy) {
+                const int ey = int(y - (s.head + int64_t(i) * EPV));
+#pragma unroll
+                for (int e = 0; e < EPV; ++e)
+                    if (e == ey) f[e] = gy;
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(DT::pack(f), rout, launder_int(voff) + (NV + kk) * nthr * 16, 0,
+                                                   kAuxNT);
+        }
     }
 
     if (tid == 0) {
@@ -287,6 +342,8 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_finalize(trlx_ilql_args a)
 }
 
 // ------------------------------------------------------------------ host side
+int tuning_split_lds();  // vocab_rows.hip ("split_lds")
+
 static const int kIlqlNVs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 16};
 
 // Register-resident geometry: the smallest NV that holds the row in <= 512 threads, else
@@ -341,6 +398,14 @@ static int ilql_launch_rows(const trlx_ilql_args& a, hipStream_t stream) {
     for (int h = 0; h < a.nq; ++h)
         TRLX_REQUIRE(same_phase(a.q[h], a.q_sb[h], a.q_st[h], a.dq[h], a.dq_sb[h], a.dq_st[h], a.B, a.A, es),
                      TRLX_ERR_STRIDE, "dq rows must have the q rows' 16-B phase (grad_buffer_like)");
+    if (es == 4 && tuning_split_lds() != 1) {  // long fp32 rows: split VGPR + LDS residency
+        const int64_t nvec = a.V / 4 + 1 + (kLineVecs - 1);
+        if (nvec > 512 * 16 && nvec <= 512 * (20 + 5)) {
+            hipLaunchKernelGGL((k_ilql_rows<DT, 20, 5>), dim3(unsigned(ilql_num_rows(a.B, a.L, a.A, a.nq))), dim3(512), 0,
+                               stream, a);
+            return check_launch("k_ilql_rows (split LDS)");
+        }
+    }
     int nv = 0, thr = 0;
     TRLX_REQUIRE(ilql_geometry(a.V, int(es), nv, thr), TRLX_ERR_SHAPE,
                  "vocab %lld too long for register-resident ILQL rows", (long long)a.V);

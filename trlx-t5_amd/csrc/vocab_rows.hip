@@ -498,6 +498,7 @@ static int g_stream_unroll = 0;
 static int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
 static int g_store_pol = 0;         // gradient-row stores: 0 nt (default), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1
 static int g_split_lds = 0;         // long fp32 rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
+int tuning_split_lds() { return g_split_lds; }
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
 // workgroup size.  Default: 512-thread workgroups (8 waves) -- measured on MI355X (C2,
