@@ -124,6 +124,37 @@ def test_logprobs_strided_causal_view():
                                                                             tok.reshape(-1)), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("pad", [0, 3])
+def test_lsm_bwd_split_rows_phase(dt, pad):
+    """V 50257 (the split VGPR + LDS residency kernels of both dtypes): logits rows read from
+    a wider buffer (row stride V + pad, so row starts drift against the contiguous dx rows:
+    the different-phase store path) and from a contiguous one (same phase)."""
+    g = torch.Generator().manual_seed(50 + pad)
+    B, Tn, V = 2, 7, 50257
+    full = (torch.randn(B, Tn, V + pad, generator=g) * 2).to(dt)
+    x = full[..., :V]
+    y = torch.randint(0, V, (B, Tn), generator=g)
+    y[0, 0], y[-1, -1] = 0, V - 1
+    gr = torch.randn(B, Tn, generator=g)
+    xd, yd, gd = cuda(full)[..., :V], cuda(y), cuda(gr)
+    lse = torch.empty((B, Tn), dtype=torch.float32, device=DEV)
+    lp = torch.empty((B, Tn), dtype=torch.float32, device=DEV)
+    _lib.call("trlx_lsm_gather_fwd", xd.data_ptr(), None, _lib.dtype_code(xd), B, Tn, V, xd.stride(0), xd.stride(1),
+              yd.data_ptr(), yd.stride(0), yd.stride(1), lp.data_ptr(), None, _lib.F32, lse.data_ptr(), None,
+              _lib.stream_of(xd))
+    dx = torch.full((B, Tn, V), 7.0, dtype=dt, device=DEV)
+    _lib.call("trlx_lsm_gather_bwd", xd.data_ptr(), _lib.dtype_code(xd), B, Tn, V, xd.stride(0), xd.stride(1),
+              yd.data_ptr(), yd.stride(0), yd.stride(1), lse.data_ptr(), gd.data_ptr(), _lib.F32,
+              dx.data_ptr(), dx.stride(0), dx.stride(1), _lib.stream_of(xd))
+    xf = x.float().requires_grad_(True)
+    ref_lp = orc.logprobs_from_logits(xf, y)
+    (ref_lp * gr).sum().backward()
+    torch.testing.assert_close(lp.cpu(), ref_lp.detach(), **RT32)
+    tol = dict(rtol=1e-2, atol=1e-6) if dt == torch.bfloat16 else RT32
+    torch.testing.assert_close(dx.float().cpu(), xf.grad, **tol)
+
+
 def test_logprobs_bad_label_is_nan_not_oob():
     x = torch.randn(1, 3, 100)
     y = torch.tensor([[0, 100, -1]])

@@ -138,8 +138,8 @@ __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, cons
 // LDS (32 KB per workgroup at NL = 4) instead of VGPRs, so a 512-thread workgroup fits in
 // 128 VGPRs and two rows stay in flight per CU (a 201-KB fp32 row held whole in VGPRs
 // needs 1024 threads at ~88 VGPRs: one row per CU, its load / reduce / store phases exposed).
-template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0>
-__global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL ? 4 : 1)) void k_vocab_rows(RowArgs a) {
+template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, int WPE = 4>
+__global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     typedef typename DT::elem_t E;
@@ -497,7 +497,7 @@ static int g_stream_threads = 0;
 static int g_stream_unroll = 0;
 static int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
 static int g_store_pol = 0;         // gradient-row stores: 0 nt (default), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1
-static int g_split_lds = 0;         // long fp32 rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
+static int g_split_lds = 0;         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
 int tuning_split_lds() { return g_split_lds; }
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
@@ -539,6 +539,19 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     a.order = g_row_order;
     a.spol = g_store_pol;
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
+    if constexpr (sizeof(typename DT::elem_t) == 2) {
+        // long bf16 rows (V > 32 k): 9 vectors per thread in VGPRs + 4 in LDS, 512 threads at
+        // <= 85 VGPRs -> three rows in flight per CU instead of two (C2 loss row 2.9 % faster)
+        const int64_t nvec = a.V / 8 + 1 + (kLineVecs - 1);
+        const bool want = g_split_lds == 2 || (g_split_lds == 0 && MODE != kFwd);
+        if (want && !g_row_variant && !g_resident_threads && nvec > 512 * 8 && nvec <= 512 * (9 + 4)) {
+            if (MODE == kFwd || rows_same_phase(a, 2))
+                hipLaunchKernelGGL((k_vocab_rows<DT, 9, MODE, true, false, 4, 6>), grid, dim3(512), 0, stream, a);
+            else
+                hipLaunchKernelGGL((k_vocab_rows<DT, 9, MODE, false, false, 4, 6>), grid, dim3(512), 0, stream, a);
+            return check_launch("k_vocab_rows (split LDS, bf16)");
+        }
+    }
     if constexpr (sizeof(typename DT::elem_t) == 4) {
         // long fp32 rows: 21 vectors per thread in VGPRs + 4 in LDS, 512 threads, 2 rows per CU
         const int64_t nvec = a.V / 4 + 1 + (kLineVecs - 1);
