@@ -244,3 +244,44 @@ def test_hot_path_device_state_with_decoder_lengths():
         torch.testing.assert_close(loss.cpu().reshape(()), ref["loss"], rtol=1e-5, atol=1e-6)
         okl.update(float(stats[8]), n_steps=B)
         assert c.host()["kl_coef"] == okl.value
+
+
+def test_c1_randomwalks_config_vs_oracle():
+    """configs[0], the reference's CPU-runnable case (examples/randomwalks/configs/
+    ppo_randomwalks.yml): 128 rollouts x 9 response tokens, V 23, fp32 logits, vf_coef 1.2,
+    cliprange_reward 1, adaptive KL (target 6, horizon 10000, n_steps = batch_size 100).
+    Four steps of the fused hot path with device state vs the restated orchestrator + loss +
+    controller."""
+    B, Tn, V = 128, 9, 23
+    cfg = P.PPOConfig(init_kl_coef=0.05, target=6, horizon=10000, gamma=1, lam=0.95, cliprange=0.2,
+                      cliprange_value=0.2, vf_coef=1.2, scale_reward=False, cliprange_reward=1)
+    c = P.PPOControlState.from_config(cfg, DEV, n_steps=100)
+    hp = P.PPOHotPath(cfg, B, Tn, V, torch.float32, DEV, kl_coef=0.05, ctl=c)
+    oc = orc.ScoreControl(False, 1)
+    okl = orc.AdaptiveKLController(0.05, 6, 10000)
+    g = torch.Generator().manual_seed(23)
+    for step in range(4):
+        logits, ref_logits, new_logits, labels, old_values, values = _step_inputs(B, Tn, V, 90 + step)
+        logits, ref_logits, new_logits = (t.float() * 2 for t in (logits, ref_logits, new_logits))
+        scores = torch.rand(B, generator=g) * 4 - 2  # beyond the +-1 clip on both sides
+        beta = okl.value
+        loss, stats, dl, dv = hp.step(cuda(logits), cuda(ref_logits), cuda(new_logits), cuda(labels),
+                                      cuda(old_values), cuda(values), cuda(scores))
+        torch.cuda.synchronize()
+        s_t, _, _ = oc(scores)
+        ref = orc.ppo_step_reference(logits, ref_logits, new_logits, labels, old_values, values, s_t,
+                                     cfg_kwargs=dict(vf_coef=1.2), kl_coef=beta)
+        torch.testing.assert_close(hp.lp_old.cpu(), ref["lp"], **RT32)
+        torch.testing.assert_close(hp.rewards.cpu(), ref["rewards"], **RT32, msg=f"step {step}")
+        torch.testing.assert_close(hp.returns.cpu(), ref["returns"], **RT32)
+        torch.testing.assert_close(loss.cpu().reshape(()), ref["loss"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(dl.cpu(), ref["dlogits"], rtol=1e-5, atol=1e-8)
+        torch.testing.assert_close(dv.cpu(), ref["dvalues"], rtol=1e-5, atol=1e-9)
+        st = stats.cpu().tolist()
+        for i, k in enumerate(P.STATS_KEYS):
+            assert st[i] == pytest.approx(float(ref["stats"][k]), rel=1e-5, abs=1e-6), k
+        okl.update(st[8], n_steps=100)
+        h = c.host()
+        assert h["kl_coef"] == okl.value, f"step {step}"
+        assert h["mean"] == pytest.approx(float(oc.running.mean), rel=1e-5, abs=1e-7)
+        assert h["count"] == pytest.approx(float(oc.running.count))
