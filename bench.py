@@ -62,6 +62,9 @@ def parse():
                         "experience rows)")
     p.add_argument("--tune", action="append", default=[],
                    help="key=value launch tuning (trlx_set_tuning; A/B only, results identical)")
+    p.add_argument("--global-batch", type=int, default=0,
+                   help="strong scaling: fix the GLOBAL rollout count (rows per GPU = G / N; SURVEY §8d runs C4 "
+                        "at 1024 rows on 1/2/4/8 GPUs); default 0 = the config's rows per GPU (weak scaling)")
     p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -225,6 +228,11 @@ def main():
             dist.init_process_group("gloo")
 
     B, T, V, desc = CONFIGS[args.config]
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
+        B = args.global_batch // world
+        desc = f"{desc}; strong scaling: {args.global_batch} rollouts global, {B} per GPU"
     if args.logits_dtype == "fp32" and args.config != "c5":
         desc = desc.replace("bf16 logits", "fp32 logits") + ("" if "logits" in desc else ", fp32 logits")
     ilql = args.config == "c5"
@@ -293,7 +301,7 @@ def main():
         ach = ab[dom] * tokens / (kern_ms[dom] * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and not args.global_batch:  # PMC bytes were collected at the config's rows/GPU
             with open(pmc) as f:
                 rec = json.load(f)
             traffic = rec.get(args.config + ("_fp32" if args.logits_dtype == "fp32" and not ilql else ""), {}).get(dom)
@@ -322,7 +330,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "f32",  # arithmetic type; logits_dtype in config
             "data": "synthetic",

@@ -456,3 +456,37 @@ def test_hot_path_step_fp32_logits():
     assert dlogits.dtype == torch.float32
     torch.testing.assert_close(dlogits.cpu(), ref["dlogits"], rtol=1e-4, atol=1e-9)
     torch.testing.assert_close(dvalues.cpu(), ref["dvalues"], rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("V,dt", [(50257, torch.bfloat16), (32128, torch.bfloat16), (50257, torch.float32)])
+def test_tuning_knobs_do_not_change_results(V, dt):
+    """trlx_set_tuning only changes speed: store cache policies give bit-identical rows,
+    split residency / vector order change the fp32 summation order only."""
+    B, Tn = 3, 7
+    logits, ref_logits, new_logits, labels, old_values, values, scores, _, _ = _step_inputs(B, Tn, V, 5)
+    args = [cuda(t) for t in (logits.to(dt), ref_logits.to(dt), new_logits.to(dt), labels, old_values, values,
+                              scores)]
+
+    def run():
+        hp = P.PPOHotPath(P.PPOConfig(), B, Tn, V, dt, DEV, kl_coef=0.05)
+        loss, stats, dl, dv = hp.step(*args)
+        torch.cuda.synchronize()
+        return [hp.lp_old.clone(), hp.ref_lp.clone(), loss.clone(), stats.clone(), dl.clone(), dv.clone()]
+
+    base = run()
+    try:
+        for key, vals, exact in [("store_policy", [1, 2, 3, 4, 5], True), ("split_lds", [1, 2], False),
+                                 ("row_order", [1], False), ("row_variant", [2], False)]:
+            for v in vals:
+                _lib.set_tuning(key, v)
+                got = run()
+                _lib.set_tuning(key, 0)
+                for a, b in zip(base, got):
+                    if exact:
+                        assert torch.equal(a, b), (key, v)
+                    else:
+                        tol = dict(rtol=8e-3, atol=1e-9) if b.dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-6)
+                        torch.testing.assert_close(b.float(), a.float(), **tol, msg=f"{key}={v}")
+    finally:
+        for key in ("store_policy", "split_lds", "row_order", "row_variant"):
+            _lib.set_tuning(key, 0)

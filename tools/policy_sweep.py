@@ -1,6 +1,7 @@
 """Interleaved A/B of a tuning knob on the full bench step (PPOHotPath.step as bench.py runs
 it: device controller state, overlapped loss tail).  GPU-box tool:
-    python tools/policy_sweep.py [c2|c3|c4] [knob] [values, comma-separated]"""
+    python tools/policy_sweep.py [c2|c3|c4] [knob] [values, comma-separated]
+(env: DT=fp32 for fp32 logits, ROWS=<rollouts> to override the config's rows per GPU)"""
 import os
 import sys
 import time
@@ -19,6 +20,7 @@ def main():
     knob = sys.argv[2] if len(sys.argv) > 2 else "store_policy"
     vals = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "0,1,2,3,4").split(",")]
     B, T, V, _ = bench.CONFIGS[cfg]
+    B = int(os.environ.get("ROWS", B))  # e.g. ROWS=1024 for the C4 strong-scaling shape on one GPU
     dev = torch.device("cuda:0")
     dt = torch.float32 if os.environ.get("DT") == "fp32" else torch.bfloat16
     x = bench.make_inputs(torch, B, T, V, dev, seed=1, masked=cfg == "c3", dtype=dt)

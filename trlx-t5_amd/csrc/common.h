@@ -275,6 +275,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, int(bytes), kRsrcFlags);
 }
 
+// Gradient-row store with a runtime cache policy (wave-uniform; trlx_set_tuning
+// "store_policy"): kStoreNT = nt, kStoreSC1 = sc1 (MI355X_MICROARCH.md cache-policy bits:
+// sc0 = 1, nt = 2, sc1 = 16).  nt measured best while a launch's gradient stream fits a few
+// times in the 256 MB MALL (its dirty lines drain beside the next launch's reads); sc1 for
+// multi-GB streams (C4 at 256-1024 rows: 2-5 % per step).
+enum { kStoreNT = 0, kStoreNone = 1, kStoreSC1 = 2, kStoreSC0SC1 = 3, kStoreNTSC1 = 4 };
+__device__ __forceinline__ void store_grad_b128(vec4u v, __amdgpu_buffer_rsrc_t r, int off, int spol) {
+    switch (spol) {
+        case kStoreNone: __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0); break;
+        case kStoreSC1: __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16); break;
+        case kStoreSC0SC1: __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 17); break;
+        case kStoreNTSC1: __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 18); break;
+        default: __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxNT); break;
+    }
+}
+
 // Streaming (read-once) 16-B load.
 __device__ __forceinline__ vec4u ld_stream(const vec4u* p) {
     return __builtin_nontemporal_load(p);

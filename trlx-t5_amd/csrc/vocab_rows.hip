@@ -160,11 +160,12 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(r.x + r.s.head, uint32_t(nvec) * 16u);
     const int shift = line_shift(r.x + r.s.head);  // whole 256-B spans per wave instruction
     // Vector order (tuning "row_order"): 0 = step-major (vector tid + k*nthr), 1 = wave-major
-    // (wave w owns the contiguous vectors [w*NV*64, (w+1)*NV*64)); both issue one 1-KB span
+    // (wave w owns the contiguous vectors [w*NT*64, (w+1)*NT*64), NT = NV + NL: its VGPR steps,
+    // then its LDS steps); both issue one 1-KB span
     // per wave instruction.  Both strides are runtime values, so the per-vector offsets are
     // added in VOFFSET (the raw-buffer range check covers voffset + imm, not soffset): the
     // first `shift` lanes wrap to huge offsets at k = 0 and are dropped like those past the body.
-    const int vbase = (a.order ? (tid >> 6) * (NV * kWave) + (tid & (kWave - 1)) : tid) - shift;
+    const int vbase = (a.order ? (tid >> 6) * ((NV + NL) * kWave) + (tid & (kWave - 1)) : tid) - shift;
     const int vstep = a.order ? kWave : nthr;
     const int voff = vbase * 16;
     // ---- one HBM read of the row into registers (all loads in flight at once).  Vectors
@@ -288,13 +289,7 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
             }
             const vec4u pk = DT::pack(f);
             const int off = launder_int(voff) + k * vstep * 16;
-            switch (a.spol) {  // wave-uniform; cache policy of the gradient stream
-                case 1: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 0); break;
-                case 2: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 16); break;
-                case 3: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 17); break;
-                case 4: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, 18); break;
-                default: __builtin_amdgcn_raw_buffer_store_b128(pk, rout, off, 0, kAuxNT); break;
-            }
+            store_grad_b128(pk, rout, off, a.spol);
         }
         if constexpr (NL > 0) {
 #pragma unroll
@@ -496,7 +491,18 @@ static int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 6 wave
 static int g_stream_threads = 0;
 static int g_stream_unroll = 0;
 static int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
-static int g_store_pol = 0;         // gradient-row stores: 0 nt (default), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1
+static int g_store_pol = 0;         // gradient-row stores: 0 auto, 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
+constexpr double kSC1Bytes = 1.5e9;  // auto: sc1 above this many gradient bytes per launch, else nt
+
+// Cache policy of a launch's gradient-row stores (common.h store_grad_b128).  Measured
+// (tools/policy_sweep.py, interleaved): sc1 wins on the all-VGPR rows kernel once a launch
+// writes more than ~1.5 GB (V = 32128 bf16: +1 % at 1.6 GB, +5 % at 8.4 GB) and loses on the
+// split-residency kernels at every size (V = 50257: -4 % at 1.9 / 2.5 GB) and below 1 GB.
+static int store_policy_for(double grad_bytes, bool split) {
+    if (g_store_pol == 5) return kStoreNT;
+    if (g_store_pol) return g_store_pol;
+    return (!split && grad_bytes > kSC1Bytes) ? kStoreSC1 : kStoreNT;
+}
 static int g_split_lds = 0;         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
 int tuning_split_lds() { return g_split_lds; }
 
@@ -537,7 +543,8 @@ template <int MODE, class DT>
 static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     RowArgs a = a0;
     a.order = g_row_order;
-    a.spol = g_store_pol;
+    const double grad_bytes = double(a.B) * double(a.T) * double(a.V) * double(sizeof(typename DT::elem_t));
+    a.spol = MODE == kFwd ? kStoreNT : store_policy_for(grad_bytes, true);  // split launches: LDS part nt
     const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
     if constexpr (sizeof(typename DT::elem_t) == 2) {
         // long bf16 rows (V > 32 k): 9 vectors per thread in VGPRs + 4 in LDS, 512 threads at
@@ -564,6 +571,7 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
             return check_launch("k_vocab_rows (split LDS)");
         }
     }
+    a.spol = MODE == kFwd ? kStoreNT : store_policy_for(grad_bytes, false);
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
     if (variant == 2 || g.nv == 0) {
@@ -846,7 +854,7 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
         TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "split_lds: 0..2");
         g_split_lds = int(value);
     } else if (k == "store_policy") {
-        TRLX_REQUIRE(value >= 0 && value <= 4, TRLX_ERR_ARG, "store_policy: 0..4");
+        TRLX_REQUIRE(value >= 0 && value <= 5, TRLX_ERR_ARG, "store_policy: 0..5");
         g_store_pol = int(value);
     } else if (k == "row_order") {
         TRLX_REQUIRE(value == 0 || value == 1, TRLX_ERR_ARG, "row_order: 0 or 1");
