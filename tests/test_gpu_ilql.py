@@ -217,3 +217,23 @@ def test_ilql_deterministic_and_finite_at_c5_shape():
     n = float(dones[:, :-1].sum())
     td = 2 * (Q - Qt) * dones[:, :-1].double() / n
     torch.testing.assert_close(outs[0][2].double().sum(-1), td, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("i", range(12))
+def test_ilql_random_sweep(i):
+    """Seeded random shapes: B 2..5, L 3..24, prompt 1..L-2, V 2..60000 (plus 50257 /
+    32128), one or two Q heads, fp32 / bf16, ragged rows, peaked or flat logits."""
+    import random
+    rnd = random.Random(300 + i)
+    B, L = rnd.randint(2, 5), rnd.randint(3, 24)
+    prompt = rnd.randint(1, L - 2)  # A >= 2 (A == 1 with B > 1 raises: documented deviation)
+    V = [50257, 32128][i] if i < 2 else rnd.randint(2, 60000)
+    nq = 1 + (i % 2)
+    dt = torch.bfloat16 if i % 3 == 2 else torch.float32
+    logits, qs, tqs, vs, b = make_case(B, L, V, 900 + i, dtype=dt, prompt=prompt, nq=nq, peaked=bool(i % 4 == 1))
+    got = run_gpu(P.ILQLConfig(two_qs=nq == 2), logits, qs, tqs, vs, b)
+    want = run_oracle(logits, qs, tqs, vs, b)
+    if dt == torch.bfloat16:
+        check(got, want, grad_rtol=1e-2, grad_atol=2e-6)
+    else:
+        check(got, want)
