@@ -136,3 +136,60 @@ def test_experience_from_hidden_vs_oracle():
     loss, stats, dl, dv = hp.policy_loss(new_logits, labels.to(DEV), values.to(DEV), old_values.to(DEV))
     torch.cuda.synchronize()
     assert torch.isfinite(loss).all() and torch.isfinite(dl.float()).all()
+
+
+@pytest.mark.parametrize("H,route", [(192, "gemm"), (2048, "auto"), (192, "auto")])
+def test_experience_from_hidden_routes(H, route):
+    """The GEMM route of experience_from_hidden (hipBLASLt bf16 logits + the experience rows
+    kernel; "auto" picks it from H >= LM_HEAD_GEMM_MIN_H) against the oracle on the
+    bf16-rounded logits the reference's bf16 lm_head produces (ppo_models.py:640 then
+    modeling.py:37-41), and against the fused route on the same inputs.  Tolerance: the GEMM
+    accumulates in fp32 before rounding to bf16, so a logit may land one bf16 ulp away from
+    the fp64-rounded one: atol 2e-2 (SURVEY §8c bf16 logprob bound); fused vs GEMM the same."""
+    B, T, V = 5, 7, 1031
+    g = torch.Generator().manual_seed(31 + H)
+    sc = 1.0 / H ** 0.5
+    h = (torch.randn(B, T, H, generator=g)).to(torch.bfloat16)
+    hr = (h.float() + 0.05 * torch.randn(B, T, H, generator=g)).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * sc).to(torch.bfloat16)
+    wr = (w.float() + 0.02 * sc * torch.randn(V, H, generator=g)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, T), generator=g)
+    labels[0, 0], labels[-1, -1] = 0, V - 1
+    old_values = torch.randn(B, T, generator=g)
+    scores = torch.randn(B, generator=g) * 5
+    args = [t.to(DEV) for t in (h, w, hr, wr, labels, old_values, scores)]
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    hp.experience_from_hidden(*args, route=route)
+    torch.cuda.synchronize()
+    expect_gemm = route == "gemm" or H >= P.PPOHotPath.LM_HEAD_GEMM_MIN_H
+    assert (hp.lm_logits is not None) == expect_gemm
+    lp, ref_lp, rew = hp.lp_old.cpu().double(), hp.ref_lp.cpu().double(), hp.rewards.cpu()
+    logits = (h.double() @ w.double().t()).to(torch.bfloat16).double()
+    ref_logits = (hr.double() @ wr.double().t()).to(torch.bfloat16).double()
+    o_lp = orc.logprobs_from_logits(logits, labels)
+    o_ref = orc.logprobs_from_logits(ref_logits, labels)
+    torch.testing.assert_close(lp, o_lp, rtol=0, atol=2e-2)
+    torch.testing.assert_close(ref_lp, o_ref, rtol=0, atol=2e-2)
+    torch.testing.assert_close(rew, orc.kl_penalty_rewards(lp.float(), ref_lp.float(), 0.05, scores),
+                               rtol=1e-4, atol=1e-5)
+    hf = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    hf.experience_from_hidden(*args, route="fused")
+    torch.cuda.synchronize()
+    assert hf.lm_logits is None
+    torch.testing.assert_close(hf.lp_old.cpu().double(), lp, rtol=0, atol=2e-2)
+    torch.testing.assert_close(hf.ref_lp.cpu().double(), ref_lp, rtol=0, atol=2e-2)
+
+
+def test_experience_from_hidden_route_arguments():
+    B, T, V, H = 2, 3, 67, 64
+    h = torch.zeros(B, T, H, dtype=torch.bfloat16, device=DEV)
+    w = torch.zeros(V, H, dtype=torch.bfloat16, device=DEV)
+    y = torch.zeros(B, T, dtype=torch.int64, device=DEV)
+    ov = torch.zeros(B, T, device=DEV)
+    sc = torch.zeros(B, device=DEV)
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    with pytest.raises(ValueError):
+        hp.experience_from_hidden(h, w, h, w, y, ov, sc, route="blas")
+    h32 = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.float32, DEV, kl_coef=0.05)
+    with pytest.raises(ValueError):
+        h32.experience_from_hidden(h, w, h, w, y, ov, sc, route="gemm")

@@ -52,16 +52,21 @@ def main():
             hp.experience(logits, ref_logits, y, ov, sc)
 
         def via_hidden():
+            hp.experience_from_hidden(h, w, hr, wr, y, ov, sc, route="fused")
+
+        def via_auto():  # the default dispatch (gemm route from H >= LM_HEAD_GEMM_MIN_H)
             hp.experience_from_hidden(h, w, hr, wr, y, ov, sc)
 
-        res = {"logits": [], "hidden": []}
+        res = {"logits": [], "hidden": [], "auto": []}
         for _ in range(3):
             res["logits"].append(timeit(via_logits))
             res["hidden"].append(timeit(via_hidden))
-        a, b = (sorted(v)[1] for v in res.values())
+            res["auto"].append(timeit(via_auto))
+        a, b, c = (sorted(v)[1] for v in res.values())
         flop = 2 * 2.0 * B * T * H * V
         print(f"{name:22s} B={B} T={T} H={H} V={V}: GEMMs + rows + tail {a:8.1f} us | lm_head-fused {b:8.1f} us "
-              f"({flop / b / 1e6:6.1f} TFLOP/s) | speedup {a / b:4.2f}x", flush=True)
+              f"({flop / b / 1e6:6.1f} TFLOP/s) | speedup {a / b:4.2f}x | default route {c:8.1f} us ({a / c:4.2f}x)",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -75,6 +75,7 @@ class PPOHotPath:
         self.workspace = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)  # tickets re-armed in-kernel
         self.dlogits = None
         self.lm_ws = None  # lm_head partials workspace (experience_from_hidden)
+        self.lm_logits = None  # [2, B, T, V] bf16 logits of the GEMM route (experience_from_hidden)
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
         self.timer_names = None  # optional subset of launch names to instrument (None = all)
 
@@ -120,13 +121,21 @@ class PPOHotPath:
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
         return self.lp_old, self.ref_lp
 
+    # hidden size from which the fused lm_head loses to hipBLASLt + the rows kernel
+    # (profiles/r01_experience_from_hidden.log: H = 768 fused 1.00-1.08x, H = 4096 0.92x)
+    LM_HEAD_GEMM_MIN_H = 2048
+
     def experience_from_hidden(self, hidden, weight, ref_hidden, ref_weight, labels, old_values, scores,
-                               lengths=None, mask=None, group=None):
+                               lengths=None, mask=None, group=None, route="auto"):
         """K1 with the lm_head folded in: lp / ref_lp straight from the policy's
         and the reference model's last hidden states ([B, T, H] bf16) and lm_head weights
         ([V, H] bf16) — `logits = lm_head(h)` (ppo_models.py:640, :274, :588) followed by
         logprobs_from_logits (ppo_orchestrator.py:154-155) without the [B, T, V] logits ever
-        reaching HBM (two MFMA launches, trlx_lmhead_logprobs) — then the same GAE tail."""
+        reaching HBM (two MFMA launches, trlx_lmhead_logprobs) — then the same GAE tail.
+
+        route: "fused" (above), "gemm" (hipBLASLt writes bf16 logits — the reference's own
+        bf16 lm_head output — then the experience rows kernel), or "auto" = "gemm" from
+        H >= LM_HEAD_GEMM_MIN_H on a bf16 hot path (long K, where the fused kernel is slower)."""
         B, T, V = self.B, self.T, self.V
         for h, w in ((hidden, weight), (ref_hidden, ref_weight)):
             if h.dim() != 3 or tuple(h.shape[:2]) != (B, T) or w.dim() != 2 or w.shape[0] != V or \
@@ -135,6 +144,21 @@ class PPOHotPath:
                                  f"match the hot path ({B},{T},H) x ({V},H) bf16")
         if not labels.is_contiguous():
             raise ValueError("labels must be contiguous")
+        if route not in ("auto", "fused", "gemm"):
+            raise ValueError(f"route must be auto, fused or gemm, not {route!r}")
+        if route == "gemm" and self.dtype != torch.bfloat16:
+            raise ValueError("the gemm route writes bf16 logits: it needs a bf16 hot path")
+        if route == "auto":
+            long_k = min(hidden.shape[2], ref_hidden.shape[2]) >= self.LM_HEAD_GEMM_MIN_H
+            route = "gemm" if long_k and self.dtype == torch.bfloat16 else "fused"
+        if route == "gemm":
+            _lib.require_cuda(hidden, weight, ref_hidden, ref_weight)
+            if self.lm_logits is None:
+                self.lm_logits = torch.empty((2, B, T, V), dtype=torch.bfloat16, device=self.device)
+            torch.matmul(hidden, weight.t(), out=self.lm_logits[0])
+            torch.matmul(ref_hidden, ref_weight.t(), out=self.lm_logits[1])
+            return self.experience(self.lm_logits[0], self.lm_logits[1], labels, old_values, scores,
+                                   lengths=lengths, mask=mask, group=group)
         s = torch.cuda.current_stream(self.device)
         self.distributed = dist.is_available() and dist.is_initialized()
         g_mom, work = None, None
