@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--global-batch", type=int, default=0,
                    help="strong scaling: fix the GLOBAL rollout count (rows per GPU = G / N; SURVEY §8d runs C4 "
                         "at 1024 rows on 1/2/4/8 GPUs); default 0 = the config's rows per GPU (weak scaling)")
+    p.add_argument("--loss-norm", default="rank", choices=("rank", "global"),
+                   help="PPO loss normalisers for N > 1: rank-local Σmask (the reference) or the global Σmask "
+                        "(carried by the whitening all-reduce)")
     p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -248,7 +251,8 @@ def main():
         x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
         cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
         ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
-        hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap)
+        hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap,
+                           loss_norm=args.loss_norm)
 
         def step():
             return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],

@@ -29,7 +29,7 @@ def whiten_stats_worker(rank, world, port, xs, q):
     dist.destroy_process_group()
 
 
-def hot_path_step_worker(rank, world, port, inputs, q):
+def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank"):
     """One rank of a DP PPO step on cuda:0 over gloo (the product's exchange: the whitening
     record all-reduce inside PPOHotPath.experience).  Rank r takes the contiguous row block
     r of the batch (accelerate_ppo_model.py:146-148 sharding)."""
@@ -40,7 +40,7 @@ def hot_path_step_worker(rank, world, port, inputs, q):
     dev = torch.device("cuda:0")
     sh = {k: (v.chunk(world, dim=0)[rank].contiguous().to(dev) if v is not None else None) for k, v in inputs.items()}
     B, T, V = sh["logits"].shape
-    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05)
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05, loss_norm=loss_norm)
     loss, stats, dlogits, dvalues = hp.step(sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"],
                                             sh["old_values"], sh["values"], sh["scores"], lengths=sh["lengths"],
                                             mask=sh["mask"])

@@ -125,3 +125,50 @@ def test_dp2_device_state(scale):
             kl.update(got["approx_kl"], n_steps=B // world)
             betas[r] = kl.value
             assert got["state"]["kl_coef"] == betas[r]
+
+
+def test_dp2_step_global_loss_norm():
+    """loss_norm="global" with ragged decoder lengths (unequal Σmask per rank): Σmask rides
+    the whitening all-reduce and each rank normalises by Σmask_global / W, so the DDP average
+    of the per-rank gradients is the gradient of the masked PPO loss over the CONCATENATED
+    batch (the oracle on all rows at once), and the mean of the per-rank losses is that loss
+    (SURVEY §8e global-normaliser mode; "rank" stays the reference default)."""
+    import torch.multiprocessing as mp
+    import dist_workers
+    world, B, T, V = 2, 8, 20, 1031
+    x = _inputs(B, T, V, 17, True)
+    m = x["mask"]
+    assert m[: B // 2].sum() != m[B // 2:].sum()  # the case where the two modes differ
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 150) % 300
+    ps = [ctx.Process(target=dist_workers.hot_path_step_worker, args=(r, world, port, x, q, "global"))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    f = {k: (v.float() if v is not None and v.is_floating_point() else v) for k, v in x.items()}
+    lp = orc.logprobs_from_logits(f["logits"], x["labels"])
+    ref_lp = orc.logprobs_from_logits(f["ref_logits"], x["labels"])
+    rewards = orc.kl_penalty_rewards(lp, ref_lp, 0.05, x["scores"], x["lengths"])
+    adv, ret = orc.gae(x["old_values"], rewards, T, 1.0, 0.95, use_whitening=False)
+    mu = adv.double().mean()
+    var = ((adv.double() - mu) ** 2).mean()
+    advw = ((adv.double() - mu) * torch.rsqrt(var + 1e-8)).float()
+    xg = f["new_logits"].clone().requires_grad_(True)
+    vg = x["values"].clone().requires_grad_(True)
+    new_lp = orc.logprobs_from_logits(xg, x["labels"])
+    loss, _ = orc.ppo_loss(new_lp, vg, lp, x["old_values"], advw, ret, m)
+    loss.backward()
+    for r in range(world):
+        got = res[r]
+        rows = slice(r * B // world, (r + 1) * B // world)
+        assert float(got["adv_stats"][3]) == float(m.sum()) / world
+        torch.testing.assert_close(got["dlogits"], world * xg.grad[rows], rtol=2e-2, atol=1e-6)
+        torch.testing.assert_close(got["dvalues"], world * vg.grad[rows], rtol=1e-5, atol=1e-6)
+    mean_loss = sum(res[r]["loss"].reshape(()) for r in range(world)) / world
+    torch.testing.assert_close(mean_loss, loss.detach(), rtol=1e-4, atol=1e-5)

@@ -175,3 +175,9 @@ def test_ilql_refuses_cpu_tensors():
     qs = [torch.randn(B, A, V) for _ in range(2)]
     with pytest.raises(ValueError, match="ROCm"):
         cfg.loss((torch.randn(B, L, V), (qs, qs, torch.randn(B, L, 1))), b)
+
+
+def test_hot_path_refuses_bad_loss_norm():
+    import trlx_t5_amd as P
+    with pytest.raises(ValueError):
+        P.PPOHotPath(P.PPOConfig(), 2, 3, 5, torch.bfloat16, "cpu", kl_coef=0.05, loss_norm="batch")

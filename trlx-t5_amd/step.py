@@ -25,7 +25,7 @@ overlaps the experience logits pass.
 Buffers (and the zero-filled ticket workspace) are allocated once per shape; a step
 allocates nothing.  Rows (rollouts) are sharded contiguously across ranks by the caller
 (accelerate_ppo_model.py:146-148 semantics); reference-exact loss normalisers stay
-rank-local.
+rank-local unless loss_norm="global" (Σmask then rides the whitening all-reduce).
 """
 from typing import Optional
 
@@ -44,8 +44,16 @@ __all__ = ["PPOHotPath"]
 class PPOHotPath:
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
                  device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
-                 ctl: Optional[PPOControlState] = None, overlap_tail: bool = False):
+                 ctl: Optional[PPOControlState] = None, overlap_tail: bool = False, loss_norm: str = "rank"):
         self.cfg = cfg
+        # loss_norm: "rank" = the reference's rank-local loss normalisers Σmask
+        # (ppo_models.py:162,177; DDP then averages the per-rank gradients); "global" = the
+        # whitening all-reduce also carries Σmask and each rank divides by Σmask_global / W, so
+        # the DDP-averaged gradient is that of the masked mean over the GLOBAL batch (SURVEY
+        # §8e: identical to "rank" with all-ones masks or equal Σmask per rank).
+        if loss_norm not in ("rank", "global"):
+            raise ValueError(f"loss_norm must be 'rank' or 'global', not {loss_norm!r}")
+        self.loss_norm = loss_norm
         self.B, self.T, self.V = B, T, V
         self.dtype = logits_dtype
         self.device = torch.device(device)
@@ -199,7 +207,11 @@ class PPOHotPath:
             _lib.call("trlx_ppo_rollout_gae", *tail, self.kl_coef, *outs)
         self._ev_end("rollout_gae", s)
         if self.distributed:
-            dist.all_reduce(self.adv_stats[:3], dist.ReduceOp.SUM, group=group)
+            if self.loss_norm == "global":  # {Σ A, Σ A², n, Σmask} in the same all-reduce
+                dist.all_reduce(self.adv_stats[:4], dist.ReduceOp.SUM, group=group)
+                self.adv_stats[3:4].div_(dist.get_world_size(group))
+            else:
+                dist.all_reduce(self.adv_stats[:3], dist.ReduceOp.SUM, group=group)
 
     # -------------------------------------------------------------- K2
     def policy_loss(self, new_logits, labels, values, old_values, mask=None):
