@@ -33,6 +33,8 @@ def main():
     dev = torch.device("cuda:0")
     shapes = [("C2 GPT-2 sentiments", 128, 48, 768, 50257), ("C3 T5-base", 256, 48, 768, 32128),
               ("C4 UL2-20B (per GPU)", 128, 128, 4096, 32128)]
+    if len(sys.argv) > 1:  # extra shapes "B,T,H,V ..." (route crossover sweeps)
+        shapes = [("sweep", *map(int, a.split(","))) for a in sys.argv[1:]]
     for name, B, T, H, V in shapes:
         g = torch.Generator(device=dev).manual_seed(0)
         h = (torch.randn(B, T, H, generator=g, device=dev) * 0.1).to(torch.bfloat16)

@@ -130,8 +130,9 @@ class PPOHotPath:
         return self.lp_old, self.ref_lp
 
     # hidden size from which the fused lm_head loses to hipBLASLt + the rows kernel
-    # (profiles/r01_experience_from_hidden.log: H = 768 fused 1.00-1.08x, H = 4096 0.92x)
-    LM_HEAD_GEMM_MIN_H = 2048
+    # (profiles/r01_lmhead_route_sweep.log: fused 1.00-1.08x at H <= 1024, 0.93-0.95x from
+    # H = 1536 up to UL2's 4096)
+    LM_HEAD_GEMM_MIN_H = 1280
 
     def experience_from_hidden(self, hidden, weight, ref_hidden, ref_weight, labels, old_values, scores,
                                lengths=None, mask=None, group=None, route="auto"):
