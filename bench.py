@@ -31,7 +31,9 @@ sys.path.insert(0, ROOT)
 METRIC = "PPO experience+loss tokens/sec and % HBM roofline, 1/2/4/8 MI355X"
 METRIC_ILQL = "ILQL loss (fwd+bwd) action tokens/sec and % HBM roofline, MI355X (config 5, not the headline)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level table)
-TIMER_EVERY = 10       # instrument one step in ten: HIP events around the two vocab-row launches
+TIMER_EVERY = 4        # instrument one step in four: HIP events around the vocab-row launches (>= 5 samples
+                       # in a 20-step run; a fully instrumented C2 step costs ~1.7 %, so one in four ~0.4 %)
+SETTLE_MAX_STEPS = 5000
 
 CONFIGS = {
     # name: (rows per GPU, response tokens, vocab, description)      BASELINE.json configs[]
@@ -49,7 +51,14 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--cpu-seconds", type=float, default=8.0,
+                   help="CPU baseline budget per logits dtype (0 = skip); PPO times bf16 and fp32")
+    p.add_argument("--settle-ms", type=float, default=200.0,
+                   help="after the W warm-up steps keep stepping until the GPU has been busy this long: an "
+                        "idle MI355X runs this step up to ~20%% slow for its first ~20-40 ms of load "
+                        "(profiles/r02_slowstart.log); reported as warmup_steps_run / warmup_ms (0 = off)")
+    p.add_argument("--no-fp32-line", action="store_true",
+                   help="PPO C2 at N=1: skip the secondary fp32-logits measurement (reported under fp32_logits)")
     p.add_argument("--no-timers", action="store_true", help="skip per-kernel HIP events")
     p.add_argument("--host-state", action="store_true",
                    help="PPO: keep beta as a host constant and skip the score RunningMoments/clip and the KL "
@@ -140,17 +149,27 @@ def ilql_cpu_baseline(torch, L, V, seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": toks / el, "unit": "tokens/s", "cores": cores, "kind": "port",
+    return {"value": toks / el, "unit": "tokens/s", "cores": cores, "affinity_cores": affinity_cores(), "kind": "port",
             "sample": f"{toks // (Bs * A)} steps of {Bs}x{L}x{V} fp32 (oracle.ilql_loss: reference ops incl. "
                       f"autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
 
 
-def _cores():
+def affinity_cores():
     try:
-        cores = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    return max(1, min(cores, 16))
+        return os.cpu_count() or 1
+
+
+def _cores():
+    """Threads the CPU baseline uses: every core in this process's affinity mask, unless the
+    environment caps the process's share (OMP_NUM_THREADS: the GPU box sets it to its 16-core
+    share per GPU while sched_getaffinity shows the whole machine)."""
+    cores = affinity_cores()
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    if cap.isdigit() and int(cap) > 0:
+        cores = min(cores, int(cap))
+    return max(1, cores)
 
 
 def make_inputs(torch, B, T, V, dev, seed, masked, dtype=None):
@@ -201,9 +220,114 @@ def cpu_baseline(torch, T, V, seconds, dtype=None):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": toks / el, "unit": "tokens/s", "cores": cores, "kind": "port",
+    return {"value": toks / el, "unit": "tokens/s", "cores": cores, "affinity_cores": affinity_cores(), "kind": "port",
             "sample": f"{toks // (Bs * T)} steps of {Bs}x{T}x{V} {str(bf).replace('torch.', '')} (oracle ScoreControl + ppo_step_reference + "
                       f"AdaptiveKLController: reference ops incl. autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
+
+
+def settle_and_warm(step, torch, args, dev):
+    """The W warm-up steps, then (settle) more steps until the GPU has been kept busy for
+    --settle-ms.  Measured cause (tools/slowstart_probe.py, profiles/r02_slowstart.log): after
+    an idle period (process start, or 1 s of sleep) this step runs 10-20 % slow for its first
+    ~20-40 ms of sustained load, the read-only experience launch most (244 -> 196 us), whatever
+    the buffers — a chip power/clock state, not first touch.  The queue is kept at most
+    4 steps deep (fence-free events) so the wall clock of the settle is GPU-busy time."""
+    from trlx_t5_amd.timing import LaunchEvent
+    t0 = time.perf_counter()
+    for _ in range(args.warmup):
+        step()
+    extra = 0
+    if args.settle_ms > 0:
+        ring = [LaunchEvent() for _ in range(4)]
+        s = torch.cuda.current_stream(dev)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        while (time.perf_counter() - t1) * 1e3 < args.settle_ms and extra < SETTLE_MAX_STEPS:
+            step()
+            ev = ring[extra % len(ring)]
+            ev.record(s)
+            extra += 1
+            if extra >= len(ring):  # wait for the step recorded 3 steps earlier
+                ring[extra % len(ring)].synchronize()
+    torch.cuda.synchronize()
+    return args.warmup + extra, (time.perf_counter() - t0) * 1e3
+
+
+def timed_run(step, hp, torch, dist, args, dev, world, names):
+    """Exactly K steps between barrier + synchronize pairs; max over ranks.  Per-kernel HIP
+    events (fence-free) on every TIMER_EVERY-th step, around the vocab-row launches only:
+    an event between two kernels idles the queue briefly, so instrumenting every step
+    would tax `value`."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timers = {}
+    hp.timer_names = names
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        hp.timers = timers if (not args.no_timers and i % TIMER_EVERY == TIMER_EVERY - 1) else None
+        step()
+    hp.timers = None
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, dist.ReduceOp.MAX)
+        elapsed = float(t)
+    kern_ms, samples = {}, {}
+    for name, evs in timers.items():  # HIP events on the launch stream, timed region only
+        kern_ms[name] = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        samples[name] = len(evs)
+    return elapsed, kern_ms, samples
+
+
+def pmc_traffic(key, dom):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (not measured by this run:
+    PMC needs its own rocprofv3 passes) and where they came from."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc):
+        return None, None
+    with open(pmc) as f:
+        rec = json.load(f)
+    val = rec.get(key, {}).get(dom)
+    if val is None:
+        return None, None
+    meta = rec.get("_meta", {}).get(key, {})
+    src = (f"profiles/pmc_traffic.json[{key}][{dom}]: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+           f"(FETCH x2, MI355X_MICROARCH.md §HBM) at commit {meta.get('commit', 'unrecorded')}"
+           f"{', ' + meta['command'] if 'command' in meta else ''}; not measured by this run")
+    return val, src
+
+
+def roofline(kern_ms, samples, ab, tokens, doms, elapsed, steps, traffic_key):
+    if not kern_ms:
+        return None
+    dom = max(doms, key=lambda k: kern_ms.get(k, 0.0))
+    ach = ab[dom] * tokens / (kern_ms[dom] * 1e-3) / 1e9
+    traffic, src = pmc_traffic(traffic_key, dom) if traffic_key else (None, None)
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src, "kernel": dom,
+            "bytes_per_launch": int(round(ab[dom] * tokens)), "avg_launch_us": round(kern_ms[dom] * 1e3, 2),
+            "timer_samples": samples.get(dom, 0),
+            "kernels_avg_us": {k: round(v * 1e3, 2) for k, v in kern_ms.items()},
+            "step_frac": round(ab["step"] * tokens / (elapsed / steps) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt):
+    x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
+    cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
+    ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
+    hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap,
+                      loss_norm=args.loss_norm)
+
+    def step():
+        return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],
+                       x["values"], x["scores"], lengths=x["lengths"], mask=x["mask"])
+    return hp, step, x
 
 
 def main():
@@ -246,74 +370,43 @@ def main():
 
         def step():
             return hp.step(lg, qs, tqs, vs, batch)
-    else:
-        ldt = torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16
-        x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
-        cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
-        ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
-        hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap,
-                           loss_norm=args.loss_norm)
-
-        def step():
-            return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],
-                           x["values"], x["scores"], lengths=x["lengths"], mask=x["mask"])
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # Per-kernel HIP events on every TIMER_EVERY-th step of the timed region, around the
-    # vocab-row launches only (the roofline candidates): an event record between two
-    # kernels leaves the queue idle for microseconds on this stack (measured: a fully
-    # instrumented C2 step takes ~10% longer), so instrumenting more would tax `value`.
-    timers = {}
-    hp.timer_names = {"rows"} if ilql else {"experience", "loss"}
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        hp.timers = timers if (not args.no_timers and i % TIMER_EVERY == TIMER_EVERY - 1) else None
-        step()
-    hp.timers = None
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, dist.ReduceOp.MAX)
-        elapsed = float(t)
-
-    # per-kernel average durations (HIP events on the launch stream, timed region only)
-    kern_ms = {}
-    if timers:
-        for name, evs in timers.items():
-            kern_ms[name] = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-    if ilql:  # action tokens; per-launch bytes of the rows kernel
-        tokens = B * (T - 1)
+        names = {"rows"}
+        tokens = B * (T - 1)  # action tokens; per-launch bytes of the rows kernel
         ab = {"rows": ilql_algorithmic_bytes(B, T, V, 4) / tokens}
         ab["step"] = ab["rows"]
         doms = ("rows",)
+        traffic_key = None if args.global_batch else "c5"
     else:
+        ldt = torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16
+        hp, step, x = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt)
+        names = {"experience", "loss"}
         tokens = B * T
         ab = algorithmic_bytes(V, 4 if args.logits_dtype == "fp32" else 2, masked)
         doms = ("experience", "loss")
-    roof = None
-    if kern_ms:
-        dom = max(doms, key=lambda k: kern_ms.get(k, 0.0))
-        ach = ab[dom] * tokens / (kern_ms[dom] * 1e-3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc) and not args.global_batch:  # PMC bytes were collected at the config's rows/GPU
-            with open(pmc) as f:
-                rec = json.load(f)
-            traffic = rec.get(args.config + ("_fp32" if args.logits_dtype == "fp32" and not ilql else ""), {}).get(dom)
-        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom,
-                "bytes_per_launch": int(round(ab[dom] * tokens)), "avg_launch_us": round(kern_ms[dom] * 1e3, 2),
-                "kernels_avg_us": {k: round(v * 1e3, 2) for k, v in kern_ms.items()},
-                "step_frac": round(ab["step"] * tokens / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}
+        # PMC bytes were collected at the config's rows per GPU
+        traffic_key = None if args.global_batch else args.config + ("_fp32" if args.logits_dtype == "fp32" else "")
+
+    warm_steps, warm_ms = settle_and_warm(step, torch, args, dev)
+    elapsed, kern_ms, samples = timed_run(step, hp, torch, dist, args, dev, world, names)
+    roof = roofline(kern_ms, samples, ab, tokens, doms, elapsed, args.steps, traffic_key)
+
+    # Secondary line (C2 at N=1): the same step with fp32 logits (the reference's GPT path,
+    # ppo_models.py:225-289; BASELINE.md asks for both dtypes), same K / W / settle.
+    fp32_line = None
+    if (not ilql and world == 1 and args.config == "c2" and args.logits_dtype == "bf16" and not args.no_fp32_line
+            and not args.global_batch):
+        del hp, step, x
+        torch.cuda.empty_cache()
+        hp32, step32, x32 = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, torch.float32)
+        w32, wms32 = settle_and_warm(step32, torch, args, dev)
+        el32, km32, sm32 = timed_run(step32, hp32, torch, dist, args, dev, world, names)
+        fp32_line = {"value": round(tokens * args.steps / el32, 1), "unit": "tokens/s",
+                     "ms_per_step": round(el32 / args.steps * 1e3, 4), "warmup_steps_run": w32,
+                     "warmup_ms": round(wms32, 1),
+                     "roofline": roofline(km32, sm32, algorithmic_bytes(V, 4, masked), tokens, doms, el32,
+                                          args.steps, "c2_fp32")}
+        del hp32, step32, x32
+        torch.cuda.empty_cache()
 
     out = None
     if rank == 0:
@@ -321,9 +414,12 @@ def main():
         if world == 1 and args.cpu_seconds > 0:
             if ilql:
                 cpu = ilql_cpu_baseline(torch, T, V, args.cpu_seconds)
-            else:
-                cpu = cpu_baseline(torch, T, V, args.cpu_seconds,
-                                   torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16)
+            else:  # both logits dtypes; `cpu_baseline` itself is the one matching this line
+                by = {n: cpu_baseline(torch, T, V, args.cpu_seconds, d)
+                      for n, d in (("bf16", torch.bfloat16), ("fp32", torch.float32))}
+                cpu = dict(by[args.logits_dtype])
+                cpu["by_logits_dtype"] = {n: {k: (round(v, 1) if k == "value" else v) for k, v in c.items()
+                                              if k in ("value", "sample")} for n, c in by.items()}
         ms = elapsed / args.steps * 1e3
         out = {
             "metric": METRIC_ILQL if ilql else METRIC,
@@ -332,6 +428,9 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_steps_run": warm_steps,
+            "warmup_ms": round(warm_ms, 1),
+            "settle_ms": args.settle_ms,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.global_batch else "weak",
@@ -344,6 +443,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if fp32_line:
+            out["fp32_logits"] = fp32_line
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

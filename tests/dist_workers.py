@@ -75,3 +75,34 @@ def ctl_step_worker(rank, world, port, inputs, scores_seq, scale, q):
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def drop_in_surface_worker(rank, world, port, xs_all, q):
+    """The drop-in distributed surface on cuda:0 under an initialised gloo group, exactly as
+    the reference's golden generator calls it (tests/golden/make_golden.py _dist_worker):
+    get_global_statistics / whiten / whiten(shift_mean=False) on the rank's chunk, plus
+    RunningMoments.update (modeling.py:83-104, dist branch)."""
+    import torch.distributed as dist
+    import trlx_t5_amd as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    res = {}
+    for key, xs in xs_all.items():
+        shard = xs.chunk(world, dim=0)[rank].contiguous().to(dev)
+        mean, var, count = P.get_global_statistics(shard)
+        w = P.whiten(shard)
+        w2 = P.whiten(shard, shift_mean=False)
+        wl = P.whiten(shard, distributed=False)  # the var_mean branch even with the group up
+        rm = P.RunningMoments()
+        bm, bs = rm.update(shard.float())
+        res[key] = {"mean": float(mean), "var": float(var), "count": float(count), "dtype": str(mean.dtype),
+                    # numpy (pickled by value): a torch CPU tensor would travel as a shared-memory
+                    # fd that dies with this process
+                    "whiten": w.float().cpu().numpy(), "whiten_noshift": w2.float().cpu().numpy(),
+                    "whiten_local": wl.float().cpu().numpy(),
+                    "rm": (float(rm.mean), float(rm.var), float(rm.std), float(rm.count), float(bm), float(bs))}
+    torch.cuda.synchronize()
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -193,7 +193,8 @@ def test_hot_path_device_state_needs_no_host_sync():
 def test_overlapped_loss_tail_matches_serial():
     """overlap_tail=True (the loss tail on a side stream beside the next step's experience
     rows) gives bit-identical losses, stats, gradients and controller state over several
-    steps; stats are read after wait_stats()."""
+    steps.  No wait between steps: the side-stream tail of step k really runs beside step
+    k+1's experience rows; the host waits once (wait_stats) before reading the last stats."""
     B, Tn, V = 16, 33, 3001
     outs = {}
     for overlap in (False, True):
@@ -201,18 +202,81 @@ def test_overlapped_loss_tail_matches_serial():
         c = P.PPOControlState.from_config(cfg, DEV, n_steps=B)
         hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.0, ctl=c, overlap_tail=overlap)
         g = torch.Generator().manual_seed(2)
-        rec = []
-        for step in range(4):
-            logits, ref_logits, new_logits, labels, old_values, values = [cuda(t) for t in _step_inputs(B, Tn, V, step)]
-            scores = cuda(torch.randn(B, generator=g) * 9)
-            loss, stats, dl, dv = hp.step(logits, ref_logits, new_logits, labels, old_values, values, scores)
-            hp.wait_stats()
-            rec.append((loss.clone(), stats.clone(), dl.clone(), dv.clone(), c.state.clone()))
+        inputs = [[cuda(t) for t in _step_inputs(B, Tn, V, step)] + [cuda(torch.randn(B, generator=g) * 9)]
+                  for step in range(4)]
         torch.cuda.synchronize()
-        outs[overlap] = rec
-    for a, b in zip(outs[False], outs[True]):
+        grads = []
+        for x in inputs:
+            loss, stats, dl, dv = hp.step(*x)
+            grads.append((dl.clone(), dv.clone()))  # main-stream outputs: ordered with the clone
+        hp.wait_stats()
+        outs[overlap] = (grads, loss.clone(), stats.clone(), c.state.clone())
+        torch.cuda.synchronize()
+    (ga, la, sa, ca), (gb, lb, sb, cb) = outs[False], outs[True]
+    for (x0, y0), (x1, y1) in zip(ga, gb):
+        assert torch.equal(x0, x1) and torch.equal(y0, y1)
+    assert torch.equal(la, lb) and torch.equal(sa, sb) and torch.equal(ca, cb)
+
+
+def test_overlapped_tail_several_losses_per_experience():
+    """The ppo_epochs pattern (accelerate_base_model.py:254): one experience, then several
+    policy_loss calls on it.  With overlap_tail each policy_loss must wait for the previous
+    loss tail (it rewrites the token records that tail reads): losses, stats and controller
+    state equal the serial schedule bit for bit."""
+    B, Tn, V = 12, 40, 2053
+    res = {}
+    for overlap in (False, True):
+        cfg = P.PPOConfig()
+        c = P.PPOControlState.from_config(cfg, DEV, n_steps=B)
+        hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05, ctl=c, overlap_tail=overlap)
+        logits, ref_logits, _, labels, old_values, values = [cuda(t) for t in _step_inputs(B, Tn, V, 31)]
+        news = [cuda(_step_inputs(B, Tn, V, 40 + e)[2]) for e in range(4)]
+        scores = cuda(torch.linspace(-12, 12, B))
+        hp.experience(logits, ref_logits, labels, old_values, scores)
+        rec = []
+        for e in range(4):  # no host-side wait between the updates
+            loss, stats, dl, dv = hp.policy_loss(news[e], labels, values, old_values)
+            rec.append((dl.clone(), dv.clone()))
+        hp.wait_stats()
+        # every tail advanced beta from its own approx_kl: the state carries all four
+        res[overlap] = (rec, loss.clone(), stats.clone(), c.state.clone(), c.host()["kl_updates"])
+        torch.cuda.synchronize()
+    for a, b in zip(res[False][0], res[True][0]):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+    for x, y in zip(res[False][1:4], res[True][1:4]):
+        assert torch.equal(x, y)
+    assert res[True][4] == res[False][4]
+
+
+def test_hot_path_converts_mask_and_label_dtypes():
+    """bool / int32 masks and int32 labels / lengths are converted to the int64 the kernels
+    read (not reinterpreted): the results equal the int64 inputs' bit for bit.  Float masks,
+    wrong shapes and fp64 scores are rejected."""
+    B, Tn, V = 6, 17, 509
+    g = torch.Generator().manual_seed(5)
+    logits, ref_logits, new_logits, labels, old_values, values = [cuda(t) for t in _step_inputs(B, Tn, V, 8)]
+    L = torch.randint(1, Tn + 1, (B,), generator=g)
+    mask = (torch.arange(Tn)[None, :] < L[:, None]).long()
+    old_values = old_values.masked_fill(cuda(mask) == 0, 0)
+    scores = cuda(torch.randn(B, generator=g))
+    outs = []
+    for mdt, idt in ((torch.int64, torch.int64), (torch.bool, torch.int32), (torch.int32, torch.int32)):
+        hp = P.PPOHotPath(P.PPOConfig(), B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05)
+        loss, stats, dl, dv = hp.step(logits, ref_logits, new_logits, labels.to(idt), old_values, values, scores,
+                                      lengths=cuda(L).to(idt), mask=cuda(mask).to(mdt))
+        outs.append((loss.clone(), stats.clone(), dl.clone(), dv.clone(), hp.rewards.clone()))
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
+    hp = P.PPOHotPath(P.PPOConfig(), B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05)
+    with pytest.raises(ValueError):
+        hp.step(logits, ref_logits, new_logits, labels, old_values, values, scores, mask=cuda(mask).float())
+    with pytest.raises(ValueError):
+        hp.step(logits, ref_logits, new_logits, labels[:, :-1], old_values, values, scores)
+    with pytest.raises(ValueError):
+        hp.step(logits, ref_logits, new_logits, labels, old_values, values, scores.double())
 
 
 def test_hot_path_device_state_with_decoder_lengths():

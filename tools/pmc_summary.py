@@ -2,6 +2,7 @@
 MI355X_MICROARCH.md §HBM prescribes) into per-kernel HBM bytes per launch.
 
   python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write [--config c2] [--out profiles/pmc_traffic.json]
+      [--commit <sha>] [--command '<profiled command>']
 
 Corrections (MI355X_MICROARCH.md §HBM, gfx950): FETCH_SIZE / WRITE_SIZE are in KiB;
 FETCH_SIZE reads exactly half the bytes of a wide (16 B/lane) coalesced stream -> x2.
@@ -55,6 +56,10 @@ def main():
         cfg = args[args.index("--config") + 1]
     if "--out" in args:
         out = args[args.index("--out") + 1]
+    meta = {}
+    for key in ("--commit", "--command"):
+        if key in args:
+            meta[key[2:]] = args[args.index(key) + 1]
     f = load(fetch_dir)
     w = load(write_dir)
     res = {}
@@ -79,6 +84,8 @@ def main():
         prev = json.load(open(out)) if os.path.exists(out) else {}
         prev[cfg] = summary
         prev.setdefault("_detail", {})[cfg] = res
+        if meta:
+            prev.setdefault("_meta", {})[cfg] = meta
         json.dump(prev, open(out, "w"), indent=1)
 
 

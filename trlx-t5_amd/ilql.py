@@ -216,9 +216,23 @@ class ILQLHotPath:
         B, L, V, A, nq = self.B, self.L, self.V, self.A, self.nq
         if tuple(logits.shape) != (B, L, V) or logits.dtype != self.dtype or logits.stride(-1) != 1:
             raise ValueError("logits do not match the hot path shape / dtype")
-        for q in list(qs) + list(target_qs):
+        qs, target_qs = list(qs), list(target_qs)
+        if len(qs) != nq or len(target_qs) != nq:
+            raise ValueError(f"the hot path was built for {nq} Q head(s) (two_qs={self.cfg.two_qs}); got "
+                             f"{len(qs)} Q and {len(target_qs)} target-Q heads")
+        for q in qs + target_qs:
             if tuple(q.shape) != (B, A, V) or q.dtype != self.dtype or q.stride(-1) != 1:
                 raise ValueError("Q heads must be [B, L-1, V] of the logits dtype")
+        _lib.require_cuda(logits, vs, batch.rewards, *qs, *target_qs)
+        for name, t, shape in (("vs", vs, (B, A + 1)), ("batch.rewards", batch.rewards, (B, A))):
+            ok_shape = tuple(t.shape) in (shape, shape + (1,))
+            if not ok_shape or not t.is_contiguous() or t.dtype not in (torch.float32, torch.bfloat16):
+                raise ValueError(f"{name} must be a contiguous fp32/bf16 {list(shape)} tensor (got "
+                                 f"{tuple(t.shape)}/{t.dtype}, contiguous={t.is_contiguous()})")
+        for name, shape in (("input_ids", (B, L)), ("attention_mask", (B, L)), ("actions_ixs", (B, A)),
+                            ("dones", (B, A + 1))):
+            if tuple(getattr(batch, name).shape) != shape:
+                raise ValueError(f"batch.{name} has shape {tuple(getattr(batch, name).shape)}, expected {shape}")
         if self.dlogits is None or self.dlogits.stride() != logits.stride():
             self.dlogits = grad_buffer_like(logits)
             self.dq = [grad_buffer_like(q) for q in qs[:nq]]

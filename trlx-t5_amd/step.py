@@ -86,6 +86,7 @@ class PPOHotPath:
         self.lm_logits = None  # [2, B, T, V] bf16 logits of the GEMM route (experience_from_hidden)
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
         self.timer_names = None  # optional subset of launch names to instrument (None = all)
+        self._conv = {}  # int64 buffers for labels / mask / lengths given in another integer dtype
 
     # -------------------------------------------------------------- helpers
     def _ev(self, name, s):
@@ -107,6 +108,47 @@ class PPOHotPath:
         if tuple(logits.shape) != (self.B, self.T, self.V) or logits.dtype != self.dtype or logits.stride(-1) != 1:
             raise ValueError(f"logits {tuple(logits.shape)}/{logits.dtype} do not match the hot path "
                              f"({self.B},{self.T},{self.V})/{self.dtype}")
+        if logits.device != self.device:
+            raise ValueError(f"logits on {logits.device}, hot path on {self.device}")
+
+    def _int64(self, t, shape, name, required=True):
+        """The kernels read labels / mask / lengths as contiguous int64 on this device.  int64
+        inputs pass through; other integer or bool dtypes (a bool or int32 attention mask) are
+        converted into a buffer owned by the hot path (allocated once, refilled per call)."""
+        if t is None:
+            if required:
+                raise ValueError(f"{name} is required")
+            return None
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+        if t.device != self.device:
+            raise ValueError(f"{name} on {t.device}, hot path on {self.device}")
+        if t.is_floating_point() or t.is_complex():
+            raise ValueError(f"{name} must be an integer or bool tensor, not {t.dtype}")
+        if t.dtype == torch.int64 and t.is_contiguous():
+            return t
+        buf = self._conv.get(name)
+        if buf is None:
+            buf = self._conv[name] = torch.empty(tuple(shape), dtype=torch.int64, device=self.device)
+        buf.copy_(t)
+        return buf
+
+    def _vec(self, t, shape, name, dtypes=(torch.float32, torch.bfloat16)):
+        """[B, T] / [B] float vectors (values, old_values: fp32 or bf16; scores: fp32), contiguous."""
+        if t is None and name == "scores" and self.ctl is None:
+            return None  # no score term (the KL penalty alone)
+        if t is None or tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} has shape {None if t is None else tuple(t.shape)}, expected {tuple(shape)}")
+        if t.device != self.device or not t.is_contiguous() or t.dtype not in dtypes:
+            raise ValueError(f"{name} must be a contiguous {'/'.join(str(d)[6:] for d in dtypes)} tensor on "
+                             f"{self.device} (got {t.dtype}, contiguous={t.is_contiguous()}, {t.device})")
+        return t
+
+    def _rollout_inputs(self, labels, lengths, mask, old_values, scores):
+        B, T = self.B, self.T
+        return (self._int64(labels, (B, T), "labels"), self._int64(lengths, (B,), "lengths", required=False),
+                self._int64(mask, (B, T), "mask", required=False), self._vec(old_values, (B, T), "old_values"),
+                self._vec(scores, (B,), "scores", (torch.float32,)))
 
     # -------------------------------------------------------------- K1
     def experience(self, logits, ref_logits, labels, old_values, scores, lengths=None, mask=None, group=None):
@@ -115,8 +157,9 @@ class PPOHotPath:
         self._check(ref_logits)
         if logits.stride() != ref_logits.stride():
             raise ValueError("policy and reference logits must share strides")
-        s = torch.cuda.current_stream(self.device)
         B, T, V = self.B, self.T, self.V
+        labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
+        s = torch.cuda.current_stream(self.device)
         self.distributed = dist.is_available() and dist.is_initialized()
         g_mom, work = None, None
         if self.ctl is not None:  # score moments all-reduce overlaps the logits pass
@@ -144,15 +187,20 @@ class PPOHotPath:
 
         route: "fused" (above), "gemm" (hipBLASLt writes bf16 logits — the reference's own
         bf16 lm_head output — then the experience rows kernel), or "auto" = "gemm" from
-        H >= LM_HEAD_GEMM_MIN_H on a bf16 hot path (long K, where the fused kernel is slower)."""
+        H >= LM_HEAD_GEMM_MIN_H on a bf16 hot path (long K, where the fused kernel is slower).
+
+        Rounding differs by route: "gemm" rounds every logit to bf16 before the log-softmax, as
+        the reference's bf16 lm_head does (ppo_models.py:615,640); "fused" keeps the fp32 MFMA
+        accumulator (closer to exact).  lp therefore moves by up to ~1 bf16 ulp of the logits
+        between the routes (tests/test_gpu_lmhead.py pins both against fp64 at realistic logit
+        scale).  The gemm route keeps a [2, B, T, V] bf16 buffer; release_lm_logits() frees it."""
         B, T, V = self.B, self.T, self.V
         for h, w in ((hidden, weight), (ref_hidden, ref_weight)):
             if h.dim() != 3 or tuple(h.shape[:2]) != (B, T) or w.dim() != 2 or w.shape[0] != V or \
                     w.shape[1] != h.shape[2] or h.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
                 raise ValueError(f"hidden {tuple(h.shape)}/{h.dtype} and weight {tuple(w.shape)}/{w.dtype} do not "
                                  f"match the hot path ({B},{T},H) x ({V},H) bf16")
-        if not labels.is_contiguous():
-            raise ValueError("labels must be contiguous")
+        labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
         if route not in ("auto", "fused", "gemm"):
             raise ValueError(f"route must be auto, fused or gemm, not {route!r}")
         if route == "gemm" and self.dtype != torch.bfloat16:
@@ -218,10 +266,18 @@ class PPOHotPath:
     def policy_loss(self, new_logits, labels, values, old_values, mask=None):
         """K2: fused logprob + PPO grads + dlogits, value loss, loss + stats."""
         self._check(new_logits)
+        B, T, V = self.B, self.T, self.V
+        labels = self._int64(labels, (B, T), "labels")
+        mask = self._int64(mask, (B, T), "mask", required=False)
+        values = self._vec(values, (B, T), "values")
+        old_values = self._vec(old_values, (B, T), "old_values")
         if self.dlogits is None or self.dlogits.stride() != new_logits.stride():
             self.dlogits = grad_buffer_like(new_logits)
         s = torch.cuda.current_stream(self.device)
-        B, T, V = self.B, self.T, self.V
+        if self.tail_done is not None:
+            # the previous loss tail (side stream) still reads the token records / loss /
+            # stats this launch rewrites: a second policy_loss per experience (ppo_epochs)
+            self.tail_done.wait(s)
         dx = self.dlogits
         self._ev("loss", s)
         _lib.call("trlx_ppo_loss_rows", new_logits.data_ptr(), _lib.dtype_code(new_logits), B, T, V,
@@ -252,6 +308,10 @@ class PPOHotPath:
             self.tail_done.record(ts)
         return self.loss, self.stats, self.dlogits, self.dvalues
 
+    def release_lm_logits(self):
+        """Free the gemm route's resident [2, B, T, V] logits buffer (re-allocated on next use)."""
+        self.lm_logits = None
+
     def wait_stats(self, stream=None):
         """Make `stream` (default: the current one) wait for the loss / stats of the last
         step (a no-op unless overlap_tail)."""
@@ -269,9 +329,6 @@ class PPOHotPath:
         """One experience + loss pass over this rank's shard.  The loss stats are rank-local
         like the reference's (ppo_models.py:162-198 runs per rank; Accelerate logs rank 0);
         reduce_stats=True averages them over ranks with one extra all-reduce (logging)."""
-        for t in (labels, old_values, values, scores):
-            if not t.is_contiguous():
-                raise ValueError("labels / values / scores must be contiguous")
         self.experience(logits, ref_logits, labels, old_values, scores, lengths=lengths, mask=mask, group=group)
         out = self.policy_loss(new_logits, labels, values, old_values, mask=mask)
         if reduce_stats and self.distributed:

@@ -67,6 +67,10 @@ class LaunchEvent:
         own dispatch acquire / end-of-kernel release make the data visible)."""
         _check(_runtime().hipStreamWaitEvent(ctypes.c_void_p(stream.cuda_stream), self._ev, 0), "hipStreamWaitEvent")
 
+    def synchronize(self):
+        """Block the host until the work recorded before this event has finished."""
+        _check(_runtime().hipEventSynchronize(self._ev), "hipEventSynchronize")
+
     def elapsed_time(self, end: "LaunchEvent") -> float:
         """Milliseconds between this event and `end` (waits for `end`)."""
         rt = _runtime()
