@@ -77,6 +77,10 @@ def parse():
     p.add_argument("--loss-norm", default="rank", choices=("rank", "global"),
                    help="PPO loss normalisers for N > 1: rank-local Σmask (the reference) or the global Σmask "
                         "(carried by the whitening all-reduce)")
+    p.add_argument("--schedule", default="auto", choices=("auto", "serial", "pipelined"),
+                   help="PPO: serial = PPOHotPath.step per batch; pipelined = pipeline_step (the next batch's "
+                        "experience rows run while this batch's whitening all-reduce is in flight; bit-identical "
+                        "results); auto = pipelined when N > 1 (there is no all-reduce at N = 1)")
     p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -317,16 +321,19 @@ def roofline(kern_ms, samples, ab, tokens, doms, elapsed, steps, traffic_key):
             "step_frac": round(ab["step"] * tokens / (elapsed / steps) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt):
+def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1):
     x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
     cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
     ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
     hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap,
                       loss_norm=args.loss_norm)
 
+    pipelined = args.schedule == "pipelined" or (args.schedule == "auto" and world > 1)
+    fn = hp.pipeline_step if pipelined else hp.step  # pipelined: each call = E rows of one batch + loss of the last
+
     def step():
-        return hp.step(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"],
-                       x["values"], x["scores"], lengths=x["lengths"], mask=x["mask"])
+        return fn(x["logits"], x["ref_logits"], x["new_logits"], x["labels"], x["old_values"], x["values"],
+                  x["scores"], lengths=x["lengths"], mask=x["mask"])
     return hp, step, x
 
 
@@ -376,9 +383,11 @@ def main():
         ab["step"] = ab["rows"]
         doms = ("rows",)
         traffic_key = None if args.global_batch else "c5"
+        schedule = "serial"
     else:
         ldt = torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16
-        hp, step, x = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt)
+        hp, step, x = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world)
+        schedule = "pipelined" if args.schedule == "pipelined" or (args.schedule == "auto" and world > 1) else "serial"
         names = {"experience", "loss"}
         tokens = B * T
         ab = algorithmic_bytes(V, 4 if args.logits_dtype == "fp32" else 2, masked)
@@ -439,7 +448,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world, "seq_len": T, "vocab": V,
                        "logits_dtype": "fp32" if ilql else args.logits_dtype, "tokens_per_gpu_step": tokens,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "schedule": schedule},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -69,9 +69,7 @@ const char* trlx_last_error(void);
  *                       for the loss / backward (default), 1 = off, 2 = also for the forward
  *   "store_policy"      gradient-row store cache policy: 0 auto (default: nt; sc1 for all-VGPR rows
  *                       launches writing > 1.5 GB), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
- *   "lmhead_dbg"        ping-pong lm_head ablation bits for timing probes ONLY (1 no MFMA,
- *                       2 no operand DMA, 4 no fragment reads: results are garbage)
- * Results are identical up to fp32 summation order; only speed changes (except lmhead_dbg). */
+ * Results are identical up to fp32 summation order; only speed changes. */
 int trlx_set_tuning(const char* key, int64_t value);
 
 /* ---------------------------------------------------------------- A1
@@ -294,12 +292,11 @@ int trlx_ilql_loss_fused(const trlx_ilql_args* args, void* stream);   /* the thr
  * per-token combine.
  * workspace: trlx_lmhead_workspace_bytes(N, V) bytes (no initialisation needed). */
 int64_t trlx_lmhead_workspace_bytes(int64_t N, int64_t V);
-/* Kernel variant (0 = automatic: 8 for N >= 2048, else 3; 1 persistent 256x256 with 3 stages
- * in flight; 2 256x256 tiles, 2 barriers per K-step; 3 128x128 tiles; 4 = 2 with an XCD-aware
- * tile order; 5 256x256 ping-pong (two wave groups staggered by a barrier), 4 phases per
- * K-step; 6 = 5 with the XCD-aware order; 7 persistent ping-pong; 8 ping-pong, 2 phases per
- * K-step; 9 ping-pong over a 4-slot ring of 32-deep K-steps; 10 persistent form of 8).  Results identical up to fp32 summation order.  Set before sizing the workspace
- * (the vocab tile width changes it). */
+/* Kernel variant (0 = automatic: 8 for N >= 2048, else 3; 3 = 128x128 tiles, 2 barriers per
+ * K-step; 8 = 256x256 ping-pong, two wave groups staggered by a barrier, 2 phases per K-step).
+ * Other values are rejected (the round-1 variants that measured slower were removed).  Results
+ * identical up to fp32 summation order.  Set before sizing the workspace (the vocab tile width
+ * changes it). */
 int trlx_lmhead_set_variant(int variant);
 int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                          int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,

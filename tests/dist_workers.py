@@ -106,3 +106,51 @@ def drop_in_surface_worker(rank, world, port, xs_all, q):
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap):
+    """The same sequence of batches through PPOHotPath.step (serial) and
+    PPOHotPath.pipeline_step (experience of batch k+1 ahead of the loss of batch k, the
+    whitening all-reduce in flight meanwhile) on this rank's row shards.  Returns every
+    batch's outputs of both schedules (numpy, pickled by value)."""
+    import torch.distributed as dist
+    import trlx_t5_amd as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    shards = [{k: (v.chunk(world, dim=0)[rank].contiguous().to(dev) if v is not None else None)
+               for k, v in b.items()} for b in batches]
+    B, T, V = shards[0]["logits"].shape
+    res = {}
+    for mode in ("serial", "pipelined"):
+        cfg = P.PPOConfig(scale_reward="running")
+        ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B) if use_ctl else None
+        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, overlap_tail=overlap)
+        outs = []
+
+        def grab(o):
+            loss, stats, dl, dv = o
+            hp.wait_stats()
+            torch.cuda.synchronize()
+            outs.append([loss.cpu().numpy(), stats.cpu().numpy(), dl.float().cpu().numpy(), dv.cpu().numpy()])
+
+        for sh in shards:
+            args = (sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"], sh["old_values"], sh["values"],
+                    sh["scores"])
+            if mode == "serial":
+                grab(hp.step(*args, lengths=sh["lengths"], mask=sh["mask"]))
+            else:
+                o = hp.pipeline_step(*args, lengths=sh["lengths"], mask=sh["mask"])
+                if o is not None:
+                    grab(o)
+        if mode == "pipelined":
+            grab(hp.pipeline_flush())
+        # the controller state is compared after the last batch: mid-sequence snapshots differ
+        # by design (the pipelined schedule has already run batch k+1's GAE tail, which
+        # advances RunningMoments, when batch k's loss is returned)
+        hp.wait_stats()
+        torch.cuda.synchronize()
+        res[mode] = (outs, ctl.state.cpu().numpy() if use_ctl else None)
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -6,6 +6,7 @@ rank's loss / gradients match the oracle applied to its shard with the global wh
 (loss normalisers rank-local, ppo_models.py:162,177)."""
 import os
 
+import numpy as np
 import pytest
 import torch
 
@@ -172,3 +173,33 @@ def test_dp2_step_global_loss_norm():
         torch.testing.assert_close(got["dvalues"], world * vg.grad[rows], rtol=1e-5, atol=1e-6)
     mean_loss = sum(res[r]["loss"].reshape(()) for r in range(world)) / world
     torch.testing.assert_close(mean_loss, loss.detach(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("use_ctl,overlap,lengths", [(True, True, False), (False, False, True)])
+def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths):
+    """PPOHotPath.pipeline_step (the DP schedule that hides the whitening all-reduce behind
+    the next batch's experience rows) against step() over three batches at world 2:
+    losses, stats, gradients and the device controller state bit-identical per batch."""
+    import torch.multiprocessing as mp
+    import dist_workers
+    world, B, T, V = 2, 8, 21, 1031
+    batches = [_inputs(B, T, V, 40 + i, lengths) for i in range(3)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 151) % 300
+    ps = [ctx.Process(target=dist_workers.pipeline_worker, args=(r, world, port, batches, q, use_ctl, overlap))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        (ser, ser_state), (pip, pip_state) = res[r]["serial"], res[r]["pipelined"]
+        assert len(ser) == len(pip) == len(batches)
+        if use_ctl:
+            assert np.array_equal(ser_state, pip_state), f"rank {r} controller state"
+        for i, (a, b) in enumerate(zip(ser, pip)):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y, equal_nan=True), f"rank {r} batch {i}"

@@ -237,3 +237,33 @@ def test_ilql_random_sweep(i):
         check(got, want, grad_rtol=1e-2, grad_atol=2e-6)
     else:
         check(got, want)
+
+
+@pytest.mark.parametrize("B,L,V,nq,dtype", [(4, 9, 1031, 2, torch.float32), (3, 12, 4097, 1, torch.float32),
+                                            (5, 7, 50257, 2, torch.float32), (4, 10, 2053, 2, torch.bfloat16)])
+def test_ilql_hot_path_vs_oracle(B, L, V, nq, dtype):
+    """ILQLHotPath.step (the bench's C5 path: prep, rows, finalize into buffers owned by the
+    hot path, eager gradients) against the oracle's loss, stats and autograd gradients, over
+    two steps (the buffers are reused).  The offline orchestrator's layout with a 1-token
+    prompt (A = L - 1), ragged padding."""
+    logits, qs, tqs, vs, b = make_case(B, L, V, 900 + V + nq, dtype=dtype, nq=nq)
+    cfg = P.ILQLConfig(two_qs=nq == 2)
+    hp = P.ILQLHotPath(cfg, B, L, V, dtype, DEV)
+    bd = P.ILQLBatch(*(getattr(b, f).to(DEV) for f in ("input_ids", "attention_mask", "rewards", "states_ixs",
+                                                       "actions_ixs", "dones")))
+    want = run_oracle(logits, qs, tqs, vs, b)
+    for _ in range(2):
+        losses, dl, dq, dvs = hp.step(logits.to(DEV), [q.to(DEV) for q in qs], [q.to(DEV) for q in tqs],
+                                      vs.to(DEV), bd)
+        torch.cuda.synchronize()
+        got = losses.cpu()
+        wl, ws, wdl, wdq, wdv = want
+        stats = [ws[k] for k in ("loss", "loss_q", "loss_v", "loss_cql", "loss_awac")]  # ilql._SLOT order
+        torch.testing.assert_close(got, torch.stack(stats).float(), rtol=1e-5, atol=1e-6)
+        gr = dict(rtol=1e-2, atol=1e-6) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(dl.float().cpu(), wdl, **gr)
+        for a, w in zip(dq, wdq):
+            torch.testing.assert_close(a.float().cpu(), w, **gr)
+        torch.testing.assert_close(dvs.cpu(), wdv.reshape(B, L), rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError):  # head count must match the config
+        hp.step(logits.to(DEV), [q.to(DEV) for q in qs[:1]] * (3 - nq), [q.to(DEV) for q in tqs[:1]], vs.to(DEV), bd)

@@ -27,7 +27,7 @@ def timeit(fn, reps=10):
     return sorted(ts)[len(ts) // 2]
 
 
-VARIANTS = tuple(int(v) for v in os.environ.get("LM_VARIANTS", "2,1,5,7,8").split(","))
+VARIANTS = tuple(int(v) for v in os.environ.get("LM_VARIANTS", "3,8").split(","))
 
 
 def main():

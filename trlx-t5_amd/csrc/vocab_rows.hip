@@ -833,9 +833,6 @@ extern "C" int trlx_ppo_loss_fused(const void* logits, int dtype, int64_t B, int
     return trlx_ppo_rollout_loss(B, T, stats, vf_coef, loss, loss_stats, workspace, stream);
 }
 
-namespace trlx {
-void lm_set_dbg(int v);
-}
 extern "C" int trlx_set_tuning(const char* key, int64_t value) {
     const std::string k = key ? key : "";
     if (k == "row_variant") g_row_variant = int(value);
@@ -848,8 +845,6 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
         TRLX_REQUIRE(value == 0 || (value % kWave == 0 && value <= kStreamMaxThreads), TRLX_ERR_ARG,
                      "stream_threads must be a multiple of 64 <= %d", kStreamMaxThreads);
         g_stream_threads = int(value);
-    } else if (k == "lmhead_dbg") {
-        lm_set_dbg(int(value));
     } else if (k == "split_lds") {
         TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "split_lds: 0..2");
         g_split_lds = int(value);

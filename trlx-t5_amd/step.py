@@ -87,6 +87,10 @@ class PPOHotPath:
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
         self.timer_names = None  # optional subset of launch names to instrument (None = all)
         self._conv = {}  # int64 buffers for labels / mask / lengths given in another integer dtype
+        self._ar_work = None  # pending whitening all-reduce (pipelined schedule)
+        self._ar_group = None
+        self._lp_bufs = None  # pipelined schedule: two (lp_old, ref_lp) pairs
+        self._pending = None  # pipelined schedule: the loss-side inputs of the previous batch
 
     # -------------------------------------------------------------- helpers
     def _ev(self, name, s):
@@ -164,13 +168,17 @@ class PPOHotPath:
         g_mom, work = None, None
         if self.ctl is not None:  # score moments all-reduce overlaps the logits pass
             g_mom, work = self.ctl._global_moments(scores, group, async_op=True)
+        self._experience_rows(logits, ref_logits, labels, s)
+        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
+        return self.lp_old, self.ref_lp
+
+    def _experience_rows(self, logits, ref_logits, labels, s):
+        B, T, V = self.B, self.T, self.V
         self._ev("experience", s)
         _lib.call("trlx_lsm_gather_fwd", logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V,
                   logits.stride(0), logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1),
                   self.lp_old.data_ptr(), self.ref_lp.data_ptr(), _lib.F32, None, None, s.cuda_stream)
         self._ev_end("experience", s)
-        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
-        return self.lp_old, self.ref_lp
 
     # hidden size from which the fused lm_head loses to hipBLASLt + the rows kernel
     # (profiles/r01_lmhead_route_sweep.log: fused 1.00-1.08x at H <= 1024, 0.93-0.95x from
@@ -238,7 +246,8 @@ class PPOHotPath:
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
         return self.lp_old, self.ref_lp
 
-    def _experience_tail(self, s, labels, old_values, scores, lengths, mask, group, g_mom, work):
+    def _experience_tail(self, s, labels, old_values, scores, lengths, mask, group, g_mom, work,
+                         defer_allreduce=False):
         B, T = self.B, self.T
         if work is not None:
             work.wait()
@@ -256,11 +265,22 @@ class PPOHotPath:
             _lib.call("trlx_ppo_rollout_gae", *tail, self.kl_coef, *outs)
         self._ev_end("rollout_gae", s)
         if self.distributed:
-            if self.loss_norm == "global":  # {Σ A, Σ A², n, Σmask} in the same all-reduce
-                dist.all_reduce(self.adv_stats[:4], dist.ReduceOp.SUM, group=group)
-                self.adv_stats[3:4].div_(dist.get_world_size(group))
-            else:
-                dist.all_reduce(self.adv_stats[:3], dist.ReduceOp.SUM, group=group)
+            # {Σ A, Σ A², n} (+ Σmask for the global loss normaliser): the only data-path exchange
+            k = 4 if self.loss_norm == "global" else 3
+            self._ar_group = group
+            self._ar_work = dist.all_reduce(self.adv_stats[:k], dist.ReduceOp.SUM, group=group, async_op=True)
+            if not defer_allreduce:
+                self._resolve_allreduce()
+
+    def _resolve_allreduce(self):
+        """Order the current stream after the pending whitening all-reduce (RCCL: a stream
+        wait, no host sync) and finish the global loss normaliser."""
+        w, self._ar_work = self._ar_work, None
+        if w is None:
+            return
+        w.wait()
+        if self.loss_norm == "global":
+            self.adv_stats[3:4].div_(dist.get_world_size(self._ar_group))
 
     # -------------------------------------------------------------- K2
     def policy_loss(self, new_logits, labels, values, old_values, mask=None):
@@ -322,6 +342,65 @@ class PPOHotPath:
         ev = self._sync_events[self._sync_i]
         self._sync_i = (self._sync_i + 1) % len(self._sync_events)
         return ev
+
+    # -------------------------------------------------------------- pipelined schedule (DP > 1)
+    def pipeline_step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
+                      lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None):
+        """Software-pipelined step for data parallelism: the experience rows of THIS batch run
+        while the previous batch's whitening all-reduce is in flight, then the previous
+        batch's loss, then this batch's GAE tail and its all-reduce (async):
+
+            E rows(k+1) | [AR(k) in flight] -> L rows(k) + loss tail(k) -> GAE tail(k+1) -> AR(k+1) ...
+
+        Every data dependency of step() is kept (GAE(k+1) still follows loss tail(k), whose
+        KL-controller update it reads), so losses, stats, gradients and controller state are
+        bit-identical to calling step() per batch (tests/test_gpu_dist.py); only the RCCL
+        latency leaves the critical path.  Returns the PREVIOUS batch's (loss, stats,
+        dlogits, dvalues) — valid until the next call — or None on the first call;
+        pipeline_flush() runs the last pending loss.  lp_old / ref_lp are double-buffered."""
+        self._check(logits)
+        self._check(ref_logits)
+        if logits.stride() != ref_logits.stride():
+            raise ValueError("policy and reference logits must share strides")
+        self._check(new_logits)
+        B, T = self.B, self.T
+        orig = (labels, lengths, mask)
+        labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
+        values = self._vec(values, (B, T), "values")
+        # converted index tensors live in shared buffers the next call refills: keep copies
+        labels, lengths, mask = (t if t is None or t is o else t.clone() for t, o in zip((labels, lengths, mask), orig))
+        if self._lp_bufs is None:
+            self._lp_bufs = [(self.lp_old, self.ref_lp), (torch.empty_like(self.lp_old), torch.empty_like(self.ref_lp))]
+            self._pb = 0
+        prev = self._pending
+        nb = self._pb ^ 1 if prev is not None else self._pb
+        s = torch.cuda.current_stream(self.device)
+        self.distributed = dist.is_available() and dist.is_initialized()
+        g_mom, work = None, None
+        if self.ctl is not None:
+            g_mom, work = self.ctl._global_moments(scores, group, async_op=True)
+        self.lp_old, self.ref_lp = self._lp_bufs[nb]
+        self._experience_rows(logits, ref_logits, labels, s)
+        out = self._pending_loss(s)
+        self.lp_old, self.ref_lp = self._lp_bufs[nb]
+        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work, defer_allreduce=True)
+        self._pending = dict(buf=nb, new_logits=new_logits, labels=labels, values=values, old_values=old_values,
+                             mask=mask)
+        self._pb = nb
+        return out
+
+    def _pending_loss(self, s):
+        prev, self._pending = self._pending, None
+        if prev is None:
+            return None
+        self.lp_old, self.ref_lp = self._lp_bufs[prev["buf"]]
+        self._resolve_allreduce()
+        return self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
+                                mask=prev["mask"])
+
+    def pipeline_flush(self):
+        """Run the pending loss of the last pipeline_step batch; returns its outputs (or None)."""
+        return self._pending_loss(torch.cuda.current_stream(self.device))
 
     def step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
              lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None,
