@@ -66,9 +66,10 @@ def parse():
     p.add_argument("--logits-dtype", default="bf16", choices=("bf16", "fp32"),
                    help="PPO logits dtype (bf16: the T5/UL2 path and BASELINE's C2 row; fp32: the reference's GPT "
                         "path)")
-    p.add_argument("--no-overlap", action="store_true",
-                   help="PPO: run the loss tail on the main stream (default: side stream, beside the next step's "
-                        "experience rows)")
+    p.add_argument("--overlap-tail", action="store_true",
+                   help="PPO: run the loss tail on a side stream beside the next step's experience rows (measured "
+                        "~1 %% slower than the default in-stream tail: the cross-stream event waits cost more than "
+                        "the ~9 us tail, profiles/r02_schedules.log)")
     p.add_argument("--tune", action="append", default=[],
                    help="key=value launch tuning (trlx_set_tuning; A/B only, results identical)")
     p.add_argument("--global-batch", type=int, default=0,
@@ -325,7 +326,7 @@ def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1):
     x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
     cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
     ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
-    hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=not args.no_overlap,
+    hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=args.overlap_tail,
                       loss_norm=args.loss_norm)
 
     pipelined = args.schedule == "pipelined" or (args.schedule == "auto" and world > 1)

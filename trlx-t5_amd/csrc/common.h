@@ -53,6 +53,35 @@ __device__ __forceinline__ void st_any(void* p, int dtype, int64_t i, float v) {
 // v_exp_f32 computes 2^x; callers pre-scale by log2(e) (folded into an fma).
 __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Packed-fp32 helpers (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 work on two fp32 lanes per
+// instruction at the issue cost of one): the vocab-row passes scale and accumulate element
+// pairs with them, leaving one v_exp_f32 per element.  Measured on the C2 experience rows:
+// the per-element VALU work (unpack, scale, exp, accumulate) kept the SIMDs ~70 % busy, so
+// halving the scale / accumulate instructions shortens the rows at full bandwidth.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 f2_splat(float v) { return f32x2{v, v}; }
+__device__ __forceinline__ f32x2 f2_exp2(f32x2 y) { return f32x2{exp2_fast(y.x), exp2_fast(y.y)}; }
+__device__ __forceinline__ f32x2 f2_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+// Σ over one vector's elements of 2^(f·log2e + c) as a lane pair (element 2i -> .x, 2i+1 -> .y)
+template <int N>
+__device__ __forceinline__ f32x2 exp_pair_sum(const float (&f)[N], f32x2 l2e, f32x2 c) {
+    static_assert(N % 2 == 0, "pairs");
+    f32x2 s = f2_exp2(f2_fma(f32x2{f[0], f[1]}, l2e, c));
+#pragma unroll
+    for (int e = 2; e < N; e += 2) s += f2_exp2(f2_fma(f32x2{f[e], f[e + 1]}, l2e, c));
+    return s;
+}
+// f[e] <- -g · 2^(f[e]·log2e + c) in place (the softmax part of a gradient row)
+template <int N>
+__device__ __forceinline__ void neg_g_exp_pairs(float (&f)[N], f32x2 l2e, f32x2 c, f32x2 neg_g) {
+#pragma unroll
+    for (int e = 0; e < N; e += 2) {
+        const f32x2 r = neg_g * f2_exp2(f2_fma(f32x2{f[e], f[e + 1]}, l2e, c));
+        f[e] = r.x;
+        f[e + 1] = r.y;
+    }
+}
+
 // IEEE ops that must not be contracted into fma (the reference evaluates them as
 // separately rounded torch ops).
 __device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }

@@ -220,27 +220,26 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
         const float ml2e = -m * kLog2e;
-        float sum = exp2_fast(fmaf(ex, kLog2e, ml2e));
+        const f32x2 l2e2 = f2_splat(kLog2e), ml2e2 = f2_splat(ml2e), zero2 = f2_splat(0.0f);
+        // element pairs: v_pk_fma_f32 scale, v_exp_f32 per element, v_pk_add_f32 accumulate
+        f32x2 acc = {exp2_fast(fmaf(ex, kLog2e, ml2e)), 0.0f};
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             float f[EPV];
             DT::unpack(v[k], f);
-            float sk = 0.0f;
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
-            sum += (unsigned(vbase + k * vstep) < unsigned(nvec)) ? sk : 0.0f;
+            const f32x2 sk = exp_pair_sum(f, l2e2, ml2e2);
+            acc += (unsigned(vbase + k * vstep) < unsigned(nvec)) ? sk : zero2;
         }
         if constexpr (NL > 0) {
 #pragma unroll
             for (int kk = 0; kk < NL; ++kk) {
                 float f[EPV];
                 DT::unpack(lds_row[kk * 512 + tid], f);
-                float sk = 0.0f;
-#pragma unroll
-                for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
-                sum += (unsigned(vbase + (NV + kk) * vstep) < unsigned(nvec)) ? sk : 0.0f;
+                const f32x2 sk = exp_pair_sum(f, l2e2, ml2e2);
+                acc += (unsigned(vbase + (NV + kk) * vstep) < unsigned(nvec)) ? sk : zero2;
             }
         }
+        float sum = acc.x + acc.y;
         sum = block_sum(sum, sh_sum);
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
@@ -274,13 +273,13 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     if (SAME_PHASE) {
         const __amdgpu_buffer_rsrc_t rout = make_rsrc(drow + r.s.head, uint32_t(nvec) * 16u);
         const int iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? int((r.y - r.s.head) / EPV) : -1;
+        const f32x2 l2e2 = f2_splat(kLog2e), c2 = f2_splat(lse_l2e), ng2 = f2_splat(-g);
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             const int i = vbase + k * vstep;  // lanes outside the body: range-checked away
             float f[EPV];
             DT::unpack(v[k], f);
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+            neg_g_exp_pairs(f, l2e2, c2, ng2);
             if (i == iy) {  // the label's vector: onehot term
                 const int ey = int(r.y - (r.s.head + int64_t(i) * EPV));
 #pragma unroll
@@ -297,8 +296,7 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
                 const int i = vbase + (NV + kk) * vstep;
                 float f[EPV];
                 DT::unpack(lds_row[kk * 512 + tid], f);
-#pragma unroll
-                for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+                neg_g_exp_pairs(f, l2e2, c2, ng2);
                 if (i == iy) {
                     const int ey = int(r.y - (r.s.head + int64_t(i) * EPV));
 #pragma unroll
