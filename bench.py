@@ -78,6 +78,10 @@ def parse():
     p.add_argument("--loss-norm", default="rank", choices=("rank", "global"),
                    help="PPO loss normalisers for N > 1: rank-local Σmask (the reference) or the global Σmask "
                         "(carried by the whitening all-reduce)")
+    p.add_argument("--no-defer-tail", action="store_true",
+                   help="PPO serial schedule: run each loss tail as its own launch (default: folded into the next "
+                        "step's experience rows launch, PPOHotPath(defer_tail=True); the last one is flushed inside "
+                        "the timed region)")
     p.add_argument("--schedule", default="auto", choices=("auto", "serial", "pipelined"),
                    help="PPO: serial = PPOHotPath.step per batch; pipelined = pipeline_step (the next batch's "
                         "experience rows run while this batch's whitening all-reduce is in flight; bit-identical "
@@ -274,6 +278,8 @@ def timed_run(step, hp, torch, dist, args, dev, world, names):
         hp.timers = timers if (not args.no_timers and i % TIMER_EVERY == TIMER_EVERY - 1) else None
         step()
     hp.timers = None
+    if hasattr(hp, "wait_stats"):
+        hp.wait_stats()  # a deferred loss tail runs here, inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -326,10 +332,10 @@ def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1):
     x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
     cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
     ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
-    hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=args.overlap_tail,
-                      loss_norm=args.loss_norm)
-
     pipelined = args.schedule == "pipelined" or (args.schedule == "auto" and world > 1)
+    defer = not (pipelined or args.overlap_tail or args.no_defer_tail)
+    hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=args.overlap_tail,
+                      loss_norm=args.loss_norm, defer_tail=defer)
     fn = hp.pipeline_step if pipelined else hp.step  # pipelined: each call = E rows of one batch + loss of the last
 
     def step():

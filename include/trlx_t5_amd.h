@@ -402,6 +402,18 @@ int trlx_ppo_rollout_gae_ctl(int64_t B, int64_t T, const float* lp, const float*
                              void* ret, int ret_dtype, double* stats, void* workspace, void* stream);
 int trlx_ppo_rollout_loss_ctl(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
                               float* loss_stats, void* workspace, const trlx_kl_ctl* kl, void* stream);
+/* trlx_lsm_gather_fwd (the next step's experience rows) with the PREVIOUS step's loss tail
+ * (trlx_ppo_rollout_loss[_ctl] over tail_B x tail_T token records of `workspace`; kl may be
+ * NULL) folded in as the launch's first workgroups: the tail's ~9 us latency-bound
+ * reduction and its launch leave the critical path and no cross-stream event is needed.
+ * Kernels that cannot host it (the streaming rows) run the tail as its own launch first.
+ * Stream order is that of the two calls: the tail reads the token records of the loss rows
+ * launched before, the GAE tail launched after reads the KL coefficient it updates. */
+int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int64_t B, int64_t T, int64_t V,
+                                  int64_t sb, int64_t st, const int64_t* labels, int64_t lb, int64_t lt,
+                                  void* out_lp0, void* out_lp1, int out_dtype, int64_t tail_B, int64_t tail_T,
+                                  const double* tail_stats, float vf_coef, float* loss, float* loss_stats,
+                                  void* workspace, const trlx_kl_ctl* kl, void* stream);
 
 /* ---------------------------------------------------------------- autograd plumbing
  * out[i] = x[i] * (*scale) for i < n (scale: device fp32 scalar, e.g. a backward's

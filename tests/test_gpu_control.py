@@ -190,17 +190,20 @@ def test_hot_path_device_state_needs_no_host_sync():
     assert after["kl_updates"] == before["kl_updates"] + 2
 
 
-def test_overlapped_loss_tail_matches_serial():
+@pytest.mark.parametrize("mode", ["overlap", "defer"])
+def test_overlapped_loss_tail_matches_serial(mode):
     """overlap_tail=True (the loss tail on a side stream beside the next step's experience
-    rows) gives bit-identical losses, stats, gradients and controller state over several
-    steps.  No wait between steps: the side-stream tail of step k really runs beside step
+    rows) and defer_tail=True (the loss tail folded into the next step's experience rows
+    launch) give bit-identical losses, stats, gradients and controller state over several
+    steps.  No wait between steps: the tail of step k really runs beside / inside step
     k+1's experience rows; the host waits once (wait_stats) before reading the last stats."""
     B, Tn, V = 16, 33, 3001
     outs = {}
     for overlap in (False, True):
         cfg = P.PPOConfig(scale_reward="running")
         c = P.PPOControlState.from_config(cfg, DEV, n_steps=B)
-        hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.0, ctl=c, overlap_tail=overlap)
+        kw = {"overlap_tail" if mode == "overlap" else "defer_tail": overlap}
+        hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.0, ctl=c, **kw)
         g = torch.Generator().manual_seed(2)
         inputs = [[cuda(t) for t in _step_inputs(B, Tn, V, step)] + [cuda(torch.randn(B, generator=g) * 9)]
                   for step in range(4)]
@@ -218,7 +221,8 @@ def test_overlapped_loss_tail_matches_serial():
     assert torch.equal(la, lb) and torch.equal(sa, sb) and torch.equal(ca, cb)
 
 
-def test_overlapped_tail_several_losses_per_experience():
+@pytest.mark.parametrize("mode", ["overlap", "defer"])
+def test_overlapped_tail_several_losses_per_experience(mode):
     """The ppo_epochs pattern (accelerate_base_model.py:254): one experience, then several
     policy_loss calls on it.  With overlap_tail each policy_loss must wait for the previous
     loss tail (it rewrites the token records that tail reads): losses, stats and controller
@@ -228,7 +232,8 @@ def test_overlapped_tail_several_losses_per_experience():
     for overlap in (False, True):
         cfg = P.PPOConfig()
         c = P.PPOControlState.from_config(cfg, DEV, n_steps=B)
-        hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05, ctl=c, overlap_tail=overlap)
+        kw = {"overlap_tail" if mode == "overlap" else "defer_tail": overlap}
+        hp = P.PPOHotPath(cfg, B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05, ctl=c, **kw)
         logits, ref_logits, _, labels, old_values, values = [cuda(t) for t in _step_inputs(B, Tn, V, 31)]
         news = [cuda(_step_inputs(B, Tn, V, 40 + e)[2]) for e in range(4)]
         scores = cuda(torch.linspace(-12, 12, B))
@@ -349,3 +354,33 @@ def test_c1_randomwalks_config_vs_oracle():
         assert h["kl_coef"] == okl.value, f"step {step}"
         assert h["mean"] == pytest.approx(float(oc.running.mean), rel=1e-5, abs=1e-7)
         assert h["count"] == pytest.approx(float(oc.running.count))
+
+
+@pytest.mark.parametrize("dtype,V", [(torch.bfloat16, 50257), (torch.float32, 50257), (torch.bfloat16, 1031)])
+def test_deferred_tail_fold_every_rows_kernel(dtype, V):
+    """defer_tail folds the loss tail into the experience rows launch where the rows kernel
+    can host it (register-resident rows: bf16 V = 50257 and 1031) and runs it as its own
+    launch first where it cannot (fp32 V = 50257 takes the streaming forward): three steps,
+    bit-identical to the undeferred path, including the KL-controller state."""
+    B, Tn = 6, 11
+    res = []
+    for defer in (False, True):
+        cfg = P.PPOConfig()
+        c = P.PPOControlState.from_config(cfg, DEV, n_steps=B)
+        hp = P.PPOHotPath(cfg, B, Tn, V, dtype, DEV, kl_coef=0.05, ctl=c, defer_tail=defer)
+        rec = []
+        for step in range(3):
+            logits, ref_logits, new_logits, labels, old_values, values = [cuda(t) for t in
+                                                                          _step_inputs(B, Tn, V, 60 + step)]
+            logits, ref_logits, new_logits = (t.to(dtype) for t in (logits, ref_logits, new_logits))
+            scores = cuda(torch.linspace(-3, 3, B))
+            loss, stats, dl, dv = hp.step(logits, ref_logits, new_logits, labels, old_values, values, scores)
+            rec.append((hp.rewards.clone(), dl.clone(), dv.clone()))
+        hp.wait_stats()
+        torch.cuda.synchronize()
+        res.append((rec, loss.clone(), stats.clone(), c.state.clone()))
+    for a, b in zip(res[0][0], res[1][0]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    for x, y in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(x, y)

@@ -124,6 +124,9 @@ SIGNATURES = {
                                           _score_ctl_p, _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                           _c_vp]),
     "trlx_ppo_rollout_loss_ctl": (_c_int, [_c_i64, _c_i64, _c_vp, _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
+    "trlx_lsm_gather_fwd_loss_tail": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
+                                               _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_vp, _c_f,
+                                               _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
     "trlx_ilql_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_int]),
     "trlx_ilql_prep": (_c_int, [_ilql_p, _c_vp]),
     "trlx_ilql_rows": (_c_int, [_ilql_p, _c_vp]),

@@ -203,10 +203,14 @@ __device__ __forceinline__ void loss_token_terms(const LossTokenArgs& L, float* 
     rec[10] = m;
 }
 
-__global__ __launch_bounds__(kRolloutThreads) void k_rollout_loss(LossRolloutArgs L) {
-    __shared__ double red[kRolloutsPerBlock * 16];
+// The loss tail of one block of blockDim.x / 64 rollouts (one wave each), block `blk` of
+// `nblk`: fixed-order fp64 sums of the token records, one record per block, and the block
+// that arrives last emits loss + stats and applies the KL-controller update.  `red` holds
+// (blockDim.x / 64) * 16 doubles.  Runs as k_rollout_loss, or as the first blocks of the
+// next experience rows launch (k_vocab_rows, trlx_lsm_gather_fwd_loss_tail).
+__device__ __forceinline__ void loss_tail_block(const LossRolloutArgs& L, int blk, int nblk, double* red) {
     const int lane = threadIdx.x & (kWave - 1);
-    const int b = blockIdx.x * kRolloutsPerBlock + threadIdx.x / kWave;
+    const int b = blk * int(blockDim.x / kWave) + int(threadIdx.x / kWave);
     double acc[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[k] = 0.0;
@@ -232,9 +236,9 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_loss(LossRolloutArg
         }
     }
     const double rec = block_sum_multi<16>(acc, red);
-    if (publish_record_last<16>(L.ws.loss_rec + blockIdx.x * 16, rec, L.ws.tickets + 1, gridDim.x)) {
+    if (publish_record_last<16>(L.ws.loss_rec + blk * 16, rec, L.ws.tickets + 1, unsigned(nblk))) {
         __syncthreads();  // red[] reuse
-        const double tot = reduce_records<16>(L.ws.loss_rec, gridDim.x, red);
+        const double tot = reduce_records<16>(L.ws.loss_rec, nblk, red);
         __syncthreads();
         if (threadIdx.x < 16) red[threadIdx.x] = tot;
         __syncthreads();
@@ -248,6 +252,11 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_loss(LossRolloutArg
             kl_ctl_apply(L.kl, s13[8]);  // policy/approx_kl
         }
     }
+}
+
+__global__ __launch_bounds__(kRolloutThreads) void k_rollout_loss(LossRolloutArgs L) {
+    __shared__ double red[kRolloutsPerBlock * 16];
+    loss_tail_block(L, int(blockIdx.x), int(gridDim.x), red);
 }
 
 }  // namespace trlx

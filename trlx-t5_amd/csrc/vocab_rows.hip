@@ -53,6 +53,10 @@ struct RowArgs {
     // fused loss: per-token loss records + value gradient (row_tails.h)
     float* tokrec;
     LossTokenArgs ltok;
+    // forward only: the PREVIOUS step's loss tail folded into this launch as its first
+    // `tail_blocks` workgroups (trlx_lsm_gather_fwd_loss_tail); row = blockIdx.x - tail_blocks
+    int has_tail, tail_blocks;
+    LossRolloutArgs tail;
 };
 
 // ------------------------------------------------------------------ shared row pieces
@@ -65,9 +69,9 @@ struct Row {
     bool y_ok;
     RowSplit<DT> s;
     __device__ __forceinline__ Row(const RowArgs& a)
-        : row(blockIdx.x),
-          b(int64_t(blockIdx.x) / a.T),
-          t(int64_t(blockIdx.x) - (int64_t(blockIdx.x) / a.T) * a.T),
+        : row(int64_t(blockIdx.x) - a.tail_blocks),
+          b(row / a.T),
+          t(row - b * a.T),
           x(reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st),
           y(a.labels[b * a.lb + t * a.lt]),
           y_ok(y >= 0 && y < a.V),
@@ -142,6 +146,13 @@ template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, i
 __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
+    if constexpr (MODE == kFwd) {
+        if (int(blockIdx.x) < a.tail_blocks) {  // the previous step's loss tail (block-uniform branch)
+            __shared__ double tail_red[kMaxThreads / kWave * 16];
+            if (blockIdx.y == 0) loss_tail_block(a.tail, int(blockIdx.x), a.tail_blocks, tail_red);
+            return;
+        }
+    }
     typedef typename DT::elem_t E;
     constexpr int EPV = DT::kEPV;
     const int tid = threadIdx.x, nthr = blockDim.x;
@@ -537,19 +548,35 @@ static bool rows_same_phase(const RowArgs& a, size_t es) {
     return same_steps && ((reinterpret_cast<uintptr_t>(a.x0) ^ reinterpret_cast<uintptr_t>(a.dx)) & 15u) == 0;
 }
 
+// A folded loss tail needs one workgroup per (threads / 64) rollouts ahead of the rows.
+static dim3 rows_grid(RowArgs& a, int threads, int nten) {
+    a.tail_blocks = a.has_tail ? int((a.tail.B + threads / kWave - 1) / (threads / kWave)) : 0;
+    return dim3(unsigned(a.B * a.T + a.tail_blocks), unsigned(nten));
+}
+
+// Kernels that cannot host the folded loss tail run it as its own launch first.
+static int tail_standalone(RowArgs& a, hipStream_t stream) {
+    if (!a.has_tail) return TRLX_OK;
+    a.has_tail = 0;
+    a.tail_blocks = 0;
+    const unsigned nblk = unsigned((a.tail.B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
+    hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, stream, a.tail);
+    return check_launch("k_rollout_loss");
+}
+
 template <int MODE, class DT>
 static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     RowArgs a = a0;
     a.order = g_row_order;
     const double grad_bytes = double(a.B) * double(a.T) * double(a.V) * double(sizeof(typename DT::elem_t));
     a.spol = MODE == kFwd ? kStoreNT : store_policy_for(grad_bytes, true);  // split launches: LDS part nt
-    const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
     if constexpr (sizeof(typename DT::elem_t) == 2) {
         // long bf16 rows (V > 32 k): 9 vectors per thread in VGPRs + 4 in LDS, 512 threads at
         // <= 85 VGPRs -> three rows in flight per CU instead of two (C2 loss row 2.9 % faster)
         const int64_t nvec = a.V / 8 + 1 + (kLineVecs - 1);
         const bool want = g_split_lds == 2 || (g_split_lds == 0 && MODE != kFwd);
         if (want && !g_row_variant && !g_resident_threads && nvec > 512 * 8 && nvec <= 512 * (9 + 4)) {
+            const dim3 grid = rows_grid(a, 512, nten);
             if (MODE == kFwd || rows_same_phase(a, 2))
                 hipLaunchKernelGGL((k_vocab_rows<DT, 9, MODE, true, false, 4, 6>), grid, dim3(512), 0, stream, a);
             else
@@ -562,6 +589,7 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
         const int64_t nvec = a.V / 4 + 1 + (kLineVecs - 1);
         const bool want = g_split_lds == 2 || (g_split_lds == 0 && MODE != kFwd);
         if (want && !g_row_variant && !g_resident_threads && nvec > 512 * 16 && nvec <= 512 * (21 + 4)) {
+            const dim3 grid = rows_grid(a, 512, nten);
             if (MODE == kFwd || rows_same_phase(a, 4))
                 hipLaunchKernelGGL((k_vocab_rows<DT, 21, MODE, true, false, 4>), grid, dim3(512), 0, stream, a);
             else
@@ -573,6 +601,9 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
     if (variant == 2 || g.nv == 0) {
+        const int rc = tail_standalone(a, stream);
+        if (rc) return rc;
+        const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
         const int thr = g_stream_threads ? g_stream_threads : kStreamMaxThreads;
         const int unroll = g_stream_unroll ? g_stream_unroll : 4;
         if (unroll == 8)
@@ -584,6 +615,7 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
         return check_launch("k_vocab_rows_stream");
     }
     const dim3 block(g.threads);
+    const dim3 grid = rows_grid(a, g.threads, nten);
     const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
     const bool lb512 = g.threads <= 512 && g_resident_lb512;
 #define TRLX_RESIDENT_CASE(N)                                                                          \
@@ -653,6 +685,30 @@ extern "C" int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype, in
     a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype; a.lse0 = out_lse0; a.lse1 = out_lse1;
     if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;  // empty batch: nothing to launch
     int rc = check_rows(a, dtype);
+    if (rc) return rc;
+    TRLX_REQUIRE(out_lp0 && (!x1 || out_lp1), TRLX_ERR_ARG, "NULL logprob output");
+    TRLX_REQUIRE(out_dtype == TRLX_F32 || out_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "out dtype");
+    return launch_rows<kFwd>(a, dtype, x1 ? 2 : 1, (hipStream_t)stream);
+}
+
+static int fill_loss_tail(LossRolloutArgs* L, int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                          float* loss_stats, void* workspace, const trlx_kl_ctl* kl);
+
+extern "C" int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int64_t B, int64_t T,
+                                             int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
+                                             int64_t lt, void* out_lp0, void* out_lp1, int out_dtype, int64_t tail_B,
+                                             int64_t tail_T, const double* tail_stats, float vf_coef, float* loss,
+                                             float* loss_stats, void* workspace, const trlx_kl_ctl* kl,
+                                             void* stream) {
+    RowArgs a = {};
+    a.x0 = x0; a.x1 = x1; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
+    a.labels = labels; a.lb = lb; a.lt = lt;
+    a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype;
+    int rc = fill_loss_tail(&a.tail, tail_B, tail_T, tail_stats, vf_coef, loss, loss_stats, workspace, kl);
+    if (rc) return rc;
+    a.has_tail = 1;
+    if (B * T == 0 && B >= 0 && T >= 0) return tail_standalone(a, (hipStream_t)stream);
+    rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(out_lp0 && (!x1 || out_lp1), TRLX_ERR_ARG, "NULL logprob output");
     TRLX_REQUIRE(out_dtype == TRLX_F32 || out_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "out dtype");
@@ -785,21 +841,29 @@ extern "C" int trlx_ppo_loss_rows(const void* logits, int dtype, int64_t B, int6
     return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
 }
 
-static int rollout_loss_impl(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
-                             float* loss_stats, void* workspace, const trlx_kl_ctl* kl, void* stream) {
+static int fill_loss_tail(LossRolloutArgs* L, int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                          float* loss_stats, void* workspace, const trlx_kl_ctl* kl) {
     TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
-    TRLX_REQUIRE(loss && loss_stats && workspace, TRLX_ERR_ARG, "NULL argument to trlx_ppo_rollout_loss");
-    LossRolloutArgs L = {};
-    carve_workspace(workspace, B, T, &L.ws);
-    L.B = int(B); L.T = int(T); L.msum = stats ? stats + 3 : nullptr; L.vf_coef = vf_coef; L.loss = loss;
-    L.stats = loss_stats;
+    TRLX_REQUIRE(loss && loss_stats && workspace, TRLX_ERR_ARG, "NULL argument to the PPO loss tail");
+    *L = {};
+    carve_workspace(workspace, B, T, &L->ws);
+    L->B = int(B); L->T = int(T); L->msum = stats ? stats + 3 : nullptr; L->vf_coef = vf_coef; L->loss = loss;
+    L->stats = loss_stats;
     if (kl) {
         TRLX_REQUIRE(kl->state, TRLX_ERR_ARG, "trlx_kl_ctl.state is NULL");
         TRLX_REQUIRE(!kl->adaptive || (kl->target != 0.0 && kl->horizon != 0.0), TRLX_ERR_ARG,
                      "adaptive KL control needs target and horizon");
-        L.kl.state = kl->state; L.kl.adaptive = kl->adaptive; L.kl.target = kl->target;
-        L.kl.horizon = kl->horizon; L.kl.n_steps = double(kl->n_steps);
+        L->kl.state = kl->state; L->kl.adaptive = kl->adaptive; L->kl.target = kl->target;
+        L->kl.horizon = kl->horizon; L->kl.n_steps = double(kl->n_steps);
     }
+    return TRLX_OK;
+}
+
+static int rollout_loss_impl(int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
+                             float* loss_stats, void* workspace, const trlx_kl_ctl* kl, void* stream) {
+    LossRolloutArgs L;
+    const int rc = fill_loss_tail(&L, B, T, stats, vf_coef, loss, loss_stats, workspace, kl);
+    if (rc) return rc;
     const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
     hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, L);
     return check_launch("k_rollout_loss");

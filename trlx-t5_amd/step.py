@@ -44,8 +44,17 @@ __all__ = ["PPOHotPath"]
 class PPOHotPath:
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
                  device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
-                 ctl: Optional[PPOControlState] = None, overlap_tail: bool = False, loss_norm: str = "rank"):
+                 ctl: Optional[PPOControlState] = None, overlap_tail: bool = False, loss_norm: str = "rank",
+                 defer_tail: bool = False):
         self.cfg = cfg
+        # defer_tail: the loss tail of step k runs as the first workgroups of step k+1's
+        # experience rows launch (trlx_lsm_gather_fwd_loss_tail) instead of its own launch on
+        # the critical path; loss / stats / beta of the last step are final after wait_stats()
+        # (which launches a still-pending tail by itself).
+        if defer_tail and overlap_tail:
+            raise ValueError("defer_tail and overlap_tail are alternatives")
+        self.defer_tail = bool(defer_tail)
+        self._tail_pending = None
         # loss_norm: "rank" = the reference's rank-local loss normalisers Σmask
         # (ppo_models.py:162,177; DDP then averages the per-rank gradients); "global" = the
         # whitening all-reduce also carries Σmask and each rank divides by Σmask_global / W, so
@@ -174,11 +183,26 @@ class PPOHotPath:
 
     def _experience_rows(self, logits, ref_logits, labels, s):
         B, T, V = self.B, self.T, self.V
+        rows = (logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V, logits.stride(0),
+                logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1), self.lp_old.data_ptr(),
+                self.ref_lp.data_ptr(), _lib.F32)
         self._ev("experience", s)
-        _lib.call("trlx_lsm_gather_fwd", logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V,
-                  logits.stride(0), logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1),
-                  self.lp_old.data_ptr(), self.ref_lp.data_ptr(), _lib.F32, None, None, s.cuda_stream)
+        if self._tail_pending is not None:  # the previous step's loss tail rides this launch
+            pend, self._tail_pending = self._tail_pending, None
+            _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, *pend, s.cuda_stream)
+        else:
+            _lib.call("trlx_lsm_gather_fwd", *rows, None, None, s.cuda_stream)
         self._ev_end("experience", s)
+
+    def _launch_pending_tail(self, s):
+        """Run a deferred loss tail by itself (nothing to fold it into)."""
+        if self._tail_pending is None:
+            return
+        (B, T, st, vf, loss, stats, ws, kl), self._tail_pending = self._tail_pending, None
+        if kl is not None:
+            _lib.call("trlx_ppo_rollout_loss_ctl", B, T, st, vf, loss, stats, ws, kl, s.cuda_stream)
+        else:
+            _lib.call("trlx_ppo_rollout_loss", B, T, st, vf, loss, stats, ws, s.cuda_stream)
 
     # hidden size from which the fused lm_head loses to hipBLASLt + the rows kernel
     # (profiles/r01_lmhead_route_sweep.log: fused 1.00-1.08x at H <= 1024, 0.93-0.95x from
@@ -225,6 +249,7 @@ class PPOHotPath:
             return self.experience(self.lm_logits[0], self.lm_logits[1], labels, old_values, scores,
                                    lengths=lengths, mask=mask, group=group)
         s = torch.cuda.current_stream(self.device)
+        self._launch_pending_tail(s)
         self.distributed = dist.is_available() and dist.is_initialized()
         g_mom, work = None, None
         if self.ctl is not None:
@@ -294,9 +319,11 @@ class PPOHotPath:
         if self.dlogits is None or self.dlogits.stride() != new_logits.stride():
             self.dlogits = grad_buffer_like(new_logits)
         s = torch.cuda.current_stream(self.device)
+        # the previous loss tail still to read the token records / loss / stats this launch
+        # rewrites (a second policy_loss per experience, the ppo_epochs pattern): deferred ->
+        # run it now; on the side stream -> wait for it
+        self._launch_pending_tail(s)
         if self.tail_done is not None:
-            # the previous loss tail (side stream) still reads the token records / loss /
-            # stats this launch rewrites: a second policy_loss per experience (ppo_epochs)
             self.tail_done.wait(s)
         dx = self.dlogits
         self._ev("loss", s)
@@ -315,9 +342,12 @@ class PPOHotPath:
             rows_done.record(s)
             ts = self.tail_stream
             rows_done.wait(ts)
-        self._ev("rollout_loss", ts)
         args = (B, T, self.adv_stats.data_ptr(), float(self.cfg.vf_coef), self.loss.data_ptr(),
                 self.stats.data_ptr(), self.workspace.data_ptr())
+        if self.defer_tail:  # runs inside the next experience launch (or wait_stats)
+            self._tail_pending = args + ((self.ctl.kl_ctl() if self.ctl is not None else None),)
+            return self.loss, self.stats, self.dlogits, self.dvalues
+        self._ev("rollout_loss", ts)
         if self.ctl is not None:  # + kl_ctl.update(approx_kl) (accelerate_ppo_model.py:123,130-131)
             _lib.call("trlx_ppo_rollout_loss_ctl", *args, self.ctl.kl_ctl(), ts.cuda_stream)
         else:
@@ -334,9 +364,12 @@ class PPOHotPath:
 
     def wait_stats(self, stream=None):
         """Make `stream` (default: the current one) wait for the loss / stats of the last
-        step (a no-op unless overlap_tail)."""
+        step: launches a deferred loss tail on it (defer_tail), or waits for the side-stream
+        tail (overlap_tail); a no-op otherwise."""
+        s = stream or torch.cuda.current_stream(self.device)
+        self._launch_pending_tail(s)
         if self.tail_done is not None:
-            self.tail_done.wait(stream or torch.cuda.current_stream(self.device))
+            self.tail_done.wait(s)
 
     def _next_event(self):
         ev = self._sync_events[self._sync_i]
@@ -383,6 +416,7 @@ class PPOHotPath:
         self._experience_rows(logits, ref_logits, labels, s)
         out = self._pending_loss(s)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
+        self._launch_pending_tail(s)  # this batch's GAE tail reads the beta it updates
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work, defer_allreduce=True)
         self._pending = dict(buf=nb, new_logits=new_logits, labels=labels, values=values, old_values=old_values,
                              mask=mask)
