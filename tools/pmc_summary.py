@@ -30,10 +30,9 @@ def load(d):
 
 
 def kernel_key(name):
-    if "k_vocab_rows" in name and ", 0," in name:
-        return "experience"
-    if "k_vocab_rows" in name and ", 2," in name:
-        return "loss"
+    if "k_vocab_rows<" in name:  # k_vocab_rows<DT, NV, MODE, ...>: MODE 0 = experience, 2 = fused loss rows
+        mode = name.split("k_vocab_rows<", 1)[1].split(",")[2].strip()
+        return {"0": "experience", "2": "loss"}.get(mode)
     if "k_rollout_gae" in name:
         return "rollout_gae"
     if "k_rollout_loss" in name:

@@ -196,27 +196,25 @@ __global__ __launch_bounds__(NL ? 512 : kMaxThreads, NL ? 4 : 1) void k_ilql_row
 #pragma unroll
     for (int k = 0; k < NV; ++k) launder(v[k]);
     const float ml2e = -m * kLog2e;
-    float sum = exp2_fast(fmaf(ex, kLog2e, ml2e));
+    const f32x2 l2e2 = f2_splat(kLog2e), ml2e2 = f2_splat(ml2e), zero2 = f2_splat(0.0f);
+    f32x2 acc = {exp2_fast(fmaf(ex, kLog2e, ml2e)), 0.0f};  // packed pairs, as the vocab rows
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         float f[EPV];
         DT::unpack(v[k], f);
-        float sk = 0.0f;
-#pragma unroll
-        for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
-        sum += (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? sk : 0.0f;
+        const f32x2 sk = exp_pair_sum(f, l2e2, ml2e2);
+        acc += (unsigned(tid - shift + k * nthr) < unsigned(nvec)) ? sk : zero2;
     }
     if constexpr (NL > 0) {
 #pragma unroll
         for (int kk = 0; kk < NL; ++kk) {
             float f[EPV];
             DT::unpack(lds_row[kk * 512 + tid], f);
-            float sk = 0.0f;
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) sk += exp2_fast(fmaf(f[e], kLog2e, ml2e));
-            sum += (unsigned(tid - shift + (NV + kk) * nthr) < unsigned(nvec)) ? sk : 0.0f;
+            const f32x2 sk = exp_pair_sum(f, l2e2, ml2e2);
+            acc += (unsigned(tid - shift + (NV + kk) * nthr) < unsigned(nvec)) ? sk : zero2;
         }
     }
+    float sum = acc.x + acc.y;
     sum = block_sum(sum, sh_sum);
 #pragma unroll
     for (int k = 0; k < NV; ++k) launder(v[k]);
@@ -235,13 +233,13 @@ __global__ __launch_bounds__(NL ? 512 : kMaxThreads, NL ? 4 : 1) void k_ilql_row
     if (je >= 0) DT::store1(dx, je, je == y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
     const __amdgpu_buffer_rsrc_t rout = make_rsrc(dx + s.head, uint32_t(nvec) * 16u);
     const int iy = y_ok && y >= s.head && y < s.tail0 ? int((y - s.head) / EPV) : -1;
+    const f32x2 c2 = f2_splat(lse_l2e), ng2 = f2_splat(-g);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int i = tid - shift + k * nthr;  // lanes outside the body: range-checked away
         float f[EPV];
         DT::unpack(v[k], f);
-#pragma unroll
-        for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+        neg_g_exp_pairs(f, l2e2, c2, ng2);
         if (i == iy) {
             const int ey = int(y - (s.head + int64_t(i) * EPV));
 #pragma unroll
@@ -256,8 +254,7 @@ __global__ __launch_bounds__(NL ? 512 : kMaxThreads, NL ? 4 : 1) void k_ilql_row
             const int i = tid - shift + (NV + kk) * nthr;
             float f[EPV];
             DT::unpack(lds_row[kk * 512 + tid], f);
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+            neg_g_exp_pairs(f, l2e2, c2, ng2);
             if (i == iy) {
                 const int ey = int(y - (s.head + int64_t(i) * EPV));
 #pragma unroll

@@ -410,13 +410,14 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
             if (nm == -INFINITY) continue;
             sum *= exp2_fast((m - nm) * kLog2e);
             const float nml2e = -nm * kLog2e;
+            f32x2 acc = {0.0f, 0.0f};  // packed pairs (v_pk_fma_f32 / v_pk_add_f32)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 float f[EPV];
                 DT::unpack(v[u], f);
-#pragma unroll
-                for (int e = 0; e < EPV; ++e) sum += exp2_fast(fmaf(f[e], kLog2e, nml2e));
+                acc += exp_pair_sum(f, f2_splat(kLog2e), f2_splat(nml2e));
             }
+            sum += acc.x + acc.y;
             m = nm;
         }
 #pragma unroll
@@ -460,8 +461,7 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
             if (i >= nvec) continue;
             float f[EPV];
             DT::unpack(v[u], f);
-#pragma unroll
-            for (int e = 0; e < EPV; ++e) f[e] = -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e));
+            neg_g_exp_pairs(f, f2_splat(kLog2e), f2_splat(lse_l2e), f2_splat(-g));
             if (same_phase) {
                 if (i == iy) {
                     const int ey = int(r.y - (r.s.head + i * EPV));
