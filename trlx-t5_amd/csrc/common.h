@@ -82,6 +82,15 @@ __device__ __forceinline__ void neg_g_exp_pairs(float (&f)[N], f32x2 l2e, f32x2 
     }
 }
 
+// Two signed 16-bit maxima per instruction (v_pk_max_i16).  Inline asm: hipcc 7.2 folds
+// __builtin_elementwise_max over bit-cast short2 vectors of one dwordx4 down to a single dword
+// (observed in the ISA), so the builtin is not used.
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_max_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // IEEE ops that must not be contracted into fma (the reference evaluates them as
 // separately rounded torch ops).
 __device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }

@@ -106,9 +106,8 @@ __device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row)
 
 // Forward epilogue: write lp (+lse).
 template <class DT>
-__device__ __forceinline__ void fwd_epilogue(const RowArgs& a, const Row<DT>& r, float xy, float lse) {
-    if (threadIdx.x == 0) {
-        const float lp = xy - lse;  // xy = x[y] (NaN for an out-of-range label), loaded early
+__device__ __forceinline__ void fwd_epilogue(const RowArgs& a, const Row<DT>& r, float lp, float lse) {
+    if (threadIdx.x == 0) {  // lp = (x[y] - max) - log Σ (NaN for an out-of-range label)
         st_any(blockIdx.y == 0 ? a.lp0 : a.lp1, a.out_dtype, r.row, lp);
         float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
         if (lse_out) lse_out[r.row] = lse;
@@ -145,6 +144,7 @@ __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, cons
 template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, int WPE = 4>
 __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
     __shared__ float sh_max[kMaxThreads / kWave];
+    __shared__ float sh_max2[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     if constexpr (MODE == kFwd) {
         if (int(blockIdx.x) < a.tail_blocks) {  // the previous step's loss tail (block-uniform branch)
@@ -201,11 +201,49 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     const int64_t je = r.edge_index();
     const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
 
-    float lse;
+    // lp = (x[y] - max) - log Σ exp(x - max), the reference's log_softmax order
+    // (x - max first, exact for bf16 rows): xy - (max + log Σ) would lose the low bits of lp
+    // to the rounding of lse when |max| is large.
+    float lse, lp = 0.0f;
     if (MODE == kBwd) {
         lse = a.lse_in[r.row];
     } else {
-        float m = ex;
+        float m;
+        bool exact = true;
+        if constexpr (sizeof(E) == 2) {
+            // Raw-bits maximum of bf16 rows, two elements per v_pk_max_i16 and no unpacking:
+            // non-negative floats order like their bit patterns read as signed int16, negative
+            // ones read as negative int16 below all of them, so for a row whose maximum is >= +0
+            // the largest bit pattern IS the maximum (a lane holding only negatives reports a
+            // wrong, smaller value, which cannot win).  Out-of-row lanes count as -0.0 (0x8000,
+            // the smallest int16).  A row whose maximum comes out negative or -0.0 re-runs the
+            // exact float pass below (block-uniform branch).  NaN / +-inf: +inf and positive
+            // NaN bit patterns exceed every finite value, so m is +inf / NaN exactly when the
+            // float pass would make lse NaN anyway.
+            constexpr uint32_t kNeg0 = 0x80008000u;  // -0.0 in both halves: the smallest int16
+            uint32_t acc = kNeg0;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+                const uint32_t p = pk_max_i16(pk_max_i16(v[k].x, v[k].y), pk_max_i16(v[k].z, v[k].w));
+                acc = pk_max_i16(acc, unsigned(vbase + k * vstep) < unsigned(nvec) ? p : kNeg0);
+            }
+            if constexpr (NL > 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's DMAs (it reads only its own)
+#pragma unroll
+                for (int kk = 0; kk < NL; ++kk) {
+                    const vec4u w = lds_row[kk * 512 + tid];
+                    const uint32_t p = pk_max_i16(pk_max_i16(w.x, w.y), pk_max_i16(w.z, w.w));
+                    acc = pk_max_i16(acc, unsigned(vbase + (NV + kk) * vstep) < unsigned(nvec) ? p : kNeg0);
+                }
+            }
+            const int mi = max(int(int16_t(acc & 0xffffu)), int(acc) >> 16);  // the two halves, sign-extended
+            m = block_max(fmaxf(__uint_as_float(uint32_t(mi) << 16), ex), sh_max);
+            exact = signbit(m) != 0;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) launder(v[k]);
+        }
+        if (exact) {
+        m = ex;
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             float f[EPV];
@@ -227,7 +265,8 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
                 m = (unsigned(vbase + (NV + kk) * vstep) < unsigned(nvec)) ? fmaxf(m, mk) : m;
             }
         }
-        m = block_max(m, sh_max);
+        m = block_max(m, sh_max2);
+        }
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
         const float ml2e = -m * kLog2e;
@@ -254,10 +293,16 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
         sum = block_sum(sum, sh_sum);
 #pragma unroll
         for (int k = 0; k < NV; ++k) launder(v[k]);
-        lse = m + logf(sum);
+        // The exponent offset ml2e = -m·log2e is rounded: each term above is 2^((x - m)·log2e + d)
+        // with d = m·log2e + ml2e, the exact residual of that product (fma, TwoProduct).  Undo
+        // it once per row (it is up to ~5e-4 at |m| ~ 1e4, far above the lp tolerance).
+        const float d = isfinite(m) ? fmaf(m, kLog2e, ml2e) : 0.0f;
+        const float lsum = logf(sum) - d * kLn2;
+        lse = m + lsum;
+        lp = (xy - m) - lsum;
     }
     if (MODE == kFwd) {
-        fwd_epilogue(a, r, xy, lse);
+        fwd_epilogue(a, r, lp, lse);
         return;
     }
 
@@ -267,15 +312,19 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     // (both reductions' barriers separate thread 0's s_ps writes from these reads)
     const PpoScalars ps = {s_ps[0], s_ps[1], s_ps[2], s_ps[3]};
     PolicyTerms pt = {1.f, 0.f, 0.f, false};
-    const float g = row_grad<MODE>(a, r.row, xy - lse, ps, pt);
+    const float g = row_grad<MODE>(a, r.row, lp, ps, pt);
 
     // ---- dlogits = g * (onehot(y) - exp(x - lse)), written once
     const float lse_l2e = -lse * kLog2e;
+    // as for the sum: 2^(x·log2e + lse_l2e) = p(x) · 2^d2, d2 the residual of the rounded
+    // offset; the per-row factor 2^-d2 rides on g
+    const float corr = isfinite(lse) ? exp2_fast(-fmaf(lse, kLog2e, lse_l2e)) : 1.0f;
+    const float ng = -g * corr;
     E* drow = reinterpret_cast<E*>(a.dx) + r.b * a.dsb + r.t * a.dst;
-    const float gy = g * (1.0f - exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
+    const float gy = g * (1.0f - corr * exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
     // edge elements first, and the token record's inputs parked in LDS (thread 0 reads them
     // back after the loop): fewer values live beside the row during the store loop
-    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : ng * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
     __shared__ float s_tok[6];
     if (MODE == kPpo && tid == 0) {
         s_tok[0] = pt.ratio; s_tok[1] = pt.lr; s_tok[2] = pt.pgmax; s_tok[3] = pt.pgclip ? 1.f : 0.f;
@@ -284,7 +333,7 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     if (SAME_PHASE) {
         const __amdgpu_buffer_rsrc_t rout = make_rsrc(drow + r.s.head, uint32_t(nvec) * 16u);
         const int iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? int((r.y - r.s.head) / EPV) : -1;
-        const f32x2 l2e2 = f2_splat(kLog2e), c2 = f2_splat(lse_l2e), ng2 = f2_splat(-g);
+        const f32x2 l2e2 = f2_splat(kLog2e), c2 = f2_splat(lse_l2e), ng2 = f2_splat(ng);
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
             const int i = vbase + k * vstep;  // lanes outside the body: range-checked away
@@ -328,7 +377,7 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
 #pragma unroll
                 for (int e = 0; e < EPV; ++e) {
                     const int64_t j = r.s.head + int64_t(i) * EPV + e;
-                    DT::store1(drow, j, j == r.y ? gy : -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
+                    DT::store1(drow, j, j == r.y ? gy : ng * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
                 }
             }
         }
@@ -342,7 +391,7 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
 #pragma unroll
                     for (int e = 0; e < EPV; ++e) {
                         const int64_t j = r.s.head + int64_t(i) * EPV + e;
-                        DT::store1(drow, j, j == r.y ? gy : -g * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
+                        DT::store1(drow, j, j == r.y ? gy : ng * exp2_fast(fmaf(f[e], kLog2e, lse_l2e)));
                     }
                 }
             }
@@ -384,7 +433,7 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
     const int64_t je = r.edge_index();
     const float ex = je >= 0 ? DT::load1(r.x, je) : -INFINITY;
 
-    float lse;
+    float lse, lsum = 0.0f, mx = 0.0f;  // kBwd: lse given, lp unused
     if (MODE == kBwd) {
         lse = a.lse_in[r.row];
     } else {
@@ -417,7 +466,8 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
                 DT::unpack(v[u], f);
                 acc += exp_pair_sum(f, f2_splat(kLog2e), f2_splat(nml2e));
             }
-            sum += acc.x + acc.y;
+            // this chunk's terms carry 2^d, d the residual of the rounded offset (see k_vocab_rows)
+            sum += (acc.x + acc.y) * exp2_fast(-fmaf(nm, kLog2e, nml2e));
             m = nm;
         }
 #pragma unroll
@@ -433,18 +483,23 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
         m = sh_m[0];
         sum = sh_s[0];
         for (int w = 1; w < nthr / kWave; ++w) online_merge(m, sum, sh_m[w], sh_s[w]);
-        lse = m + logf(sum);
+        lsum = logf(sum);
+        lse = m + lsum;
+        mx = m;
     }
     const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
+    const float lp = (xy - mx) - lsum;  // the reference's order, as in k_vocab_rows
     if (MODE == kFwd) {
-        fwd_epilogue(a, r, xy, lse);
+        fwd_epilogue(a, r, lp, lse);
         return;
     }
     PolicyTerms pt = {1.f, 0.f, 0.f, false};
-    const float g = row_grad<MODE>(a, r.row, xy - lse, ps, pt);
+    const float g = row_grad<MODE>(a, r.row, lp, ps, pt);
     const float lse_l2e = -lse * kLog2e;
+    const float corr = isfinite(lse) ? exp2_fast(-fmaf(lse, kLog2e, lse_l2e)) : 1.0f;  // as in k_vocab_rows
+    const float ng = -g * corr;
     E* drow = reinterpret_cast<E*>(a.dx) + r.b * a.dsb + r.t * a.dst;
-    const float gy = g * (1.0f - exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
+    const float gy = g * (1.0f - corr * exp2_fast(fmaf(xy, kLog2e, lse_l2e)));
     const bool same_phase = ((reinterpret_cast<uintptr_t>(drow) ^ reinterpret_cast<uintptr_t>(r.x)) & 15u) == 0;
     const int64_t iy = r.y_ok && r.y >= r.s.head && r.y < r.s.tail0 ? (r.y - r.s.head) / EPV : -1;
     vec4u* dvp = reinterpret_cast<vec4u*>(drow + r.s.head);
@@ -461,7 +516,7 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
             if (i >= nvec) continue;
             float f[EPV];
             DT::unpack(v[u], f);
-            neg_g_exp_pairs(f, f2_splat(kLog2e), f2_splat(lse_l2e), f2_splat(-g));
+            neg_g_exp_pairs(f, f2_splat(kLog2e), f2_splat(lse_l2e), f2_splat(ng));
             if (same_phase) {
                 if (i == iy) {
                     const int ey = int(r.y - (r.s.head + i * EPV));
@@ -479,7 +534,7 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
             }
         }
     }
-    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : -g * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
+    if (je >= 0) DT::store1(drow, je, je == r.y ? gy : ng * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
     if (MODE == kPpo && a.tokrec && tid == 0) {
         float vin[3];
         loss_token_inputs(a.ltok, r.row, vin);
