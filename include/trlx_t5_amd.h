@@ -67,6 +67,8 @@ const char* trlx_last_error(void);
  *   "row_order"         resident rows: 0 (default) = step-major vectors, 1 = wave-major
  *   "split_lds"         long rows (fp32 V > 32 k, bf16 V > 32 k): 0 = split VGPR + LDS residency
  *                       for the loss / backward (default), 1 = off, 2 = also for the forward
+ *   "split_mid"         mid-length bf16 rows (16k < V <= 32k) in the loss / backward: 0 auto (= 3),
+ *                       1 = all in VGPRs, 2 = 5 VGPR + 3 LDS vector steps, 3 = 6 + 2 (8 waves/SIMD)
  *   "store_policy"      gradient-row store cache policy: 0 auto (default: nt; sc1 for all-VGPR rows
  *                       launches writing > 1.5 GB), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
  * Results are identical up to fp32 summation order; only speed changes. */

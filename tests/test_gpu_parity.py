@@ -478,7 +478,8 @@ def test_tuning_knobs_do_not_change_results(V, dt):
     base = run()
     try:
         for key, vals, exact in [("store_policy", [1, 2, 3, 4, 5], True), ("split_lds", [1, 2], False),
-                                 ("row_order", [1], False), ("row_variant", [2], False)]:
+                                 ("split_mid", [1, 2, 3], False), ("row_order", [1], False),
+                                 ("row_variant", [2], False)]:
             for v in vals:
                 _lib.set_tuning(key, v)
                 got = run()
@@ -490,7 +491,7 @@ def test_tuning_knobs_do_not_change_results(V, dt):
                         tol = dict(rtol=8e-3, atol=1e-9) if b.dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-6)
                         torch.testing.assert_close(b.float(), a.float(), **tol, msg=f"{key}={v}")
     finally:
-        for key in ("store_policy", "split_lds", "row_order", "row_variant"):
+        for key in ("store_policy", "split_lds", "split_mid", "row_order", "row_variant"):
             _lib.set_tuning(key, 0)
 
 

@@ -568,6 +568,7 @@ static int store_policy_for(double grad_bytes, bool split) {
     return (!split && grad_bytes > kSC1Bytes) ? kStoreSC1 : kStoreNT;
 }
 static int g_split_lds = 0;         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
+static int g_split_mid = 0;         // mid bf16 rows (loss / backward): 0 auto (= 3), 1 off, 2 5+3, 3 6+2
 int tuning_split_lds() { return g_split_lds; }
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
@@ -637,6 +638,21 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
             else
                 hipLaunchKernelGGL((k_vocab_rows<DT, 9, MODE, false, false, 4, 6>), grid, dim3(512), 0, stream, a);
             return check_launch("k_vocab_rows (split LDS, bf16)");
+        }
+        // mid-length bf16 rows (V 16k-32k, T5/UL2's 32128) in the loss / backward: the last
+        // vector steps in LDS as well, so the row kernel fits 64 VGPRs and FOUR rows are in
+        // flight per CU (8 waves/SIMD) instead of three (tuning "split_mid": 1 off, 2 = 5 VGPR
+        // + 3 LDS steps, 3 = 6 + 2, the default: measured C4 loss rows 363 -> 341 us, C3
+        // 274 -> 247 us; 5 + 3 did not gain, profiles/r02_split_mid.log)
+        const int sm = g_split_mid ? g_split_mid : 3;
+        if (MODE != kFwd && sm > 1 && g_split_lds != 1 && !g_row_variant && !g_resident_threads &&
+            nvec > 512 * 4 && nvec <= 512 * 8 && rows_same_phase(a, 2)) {
+            const dim3 grid = rows_grid(a, 512, nten);
+            if (sm == 3)
+                hipLaunchKernelGGL((k_vocab_rows<DT, 6, MODE, true, false, 2, 8>), grid, dim3(512), 0, stream, a);
+            else
+                hipLaunchKernelGGL((k_vocab_rows<DT, 5, MODE, true, false, 3, 8>), grid, dim3(512), 0, stream, a);
+            return check_launch("k_vocab_rows (split LDS, mid bf16)");
         }
     }
     if constexpr (sizeof(typename DT::elem_t) == 4) {
@@ -968,6 +984,9 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
     } else if (k == "store_policy") {
         TRLX_REQUIRE(value >= 0 && value <= 5, TRLX_ERR_ARG, "store_policy: 0..5");
         g_store_pol = int(value);
+    } else if (k == "split_mid") {
+        TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG, "split_mid: 0..3");
+        g_split_mid = int(value);
     } else if (k == "row_order") {
         TRLX_REQUIRE(value == 0 || value == 1, TRLX_ERR_ARG, "row_order: 0 or 1");
         g_row_order = int(value);
