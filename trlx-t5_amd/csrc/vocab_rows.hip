@@ -644,7 +644,9 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
         // flight per CU (8 waves/SIMD) instead of three (tuning "split_mid": 1 off, 2 = 5 VGPR
         // + 3 LDS steps, 3 = 6 + 2, the default: measured C4 loss rows 363 -> 341 us, C3
         // 274 -> 247 us; 5 + 3 did not gain, profiles/r02_split_mid.log)
-        const int sm = g_split_mid ? g_split_mid : 3;
+        // Auto only below kSC1Bytes of gradient rows per launch: past it the all-VGPR kernel's
+        // `sc1` stores win (C4 at 1024 rollouts, 4.2 GB: 2.70 ms with them vs 2.91 ms split + nt).
+        const int sm = g_split_mid ? g_split_mid : (grad_bytes > kSC1Bytes && !g_store_pol ? 1 : 3);
         if (MODE != kFwd && sm > 1 && g_split_lds != 1 && !g_row_variant && !g_resident_threads &&
             nvec > 512 * 4 && nvec <= 512 * 8 && rows_same_phase(a, 2)) {
             const dim3 grid = rows_grid(a, 512, nten);
