@@ -58,7 +58,9 @@ typedef enum {
 int trlx_abi_version(void);
 const char* trlx_last_error(void);
 
-/* Process-wide launch tuning (0 = automatic, the default).  Keys:
+/* Launch tuning for A/B measurements (0 = automatic, the default).  The values are
+ * thread-local: they steer only the launches issued by the calling host thread, so one
+ * thread's experiment never changes another thread's kernels or summation order.  Keys:
  *   "row_variant"       1 = register-resident vocab rows, 2 = streaming vocab rows
  *   "resident_threads"  workgroup size for resident rows (multiple of 64)
  *   "resident_lb512"    1 = <=512-thread resident rows compiled for 6 waves/SIMD (default 0)

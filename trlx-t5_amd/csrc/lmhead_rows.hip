@@ -472,7 +472,7 @@ using namespace trlx;
 // persistent 3-stage form, a 4-phase ping-pong (with and without an XCD remap), persistent
 // ping-pongs and a 32-deep 4-slot ring: all slower than or tied with variant 8;
 // they were removed from the library in round 2 (git history: lmhead_rows.hip at 63d22a9).
-static int g_lm_variant = 0;
+static thread_local int g_lm_variant = 0;
 static int lm_variant(int64_t N) {
     if (g_lm_variant) return g_lm_variant;
     return N < 2048 ? 3 : 8;

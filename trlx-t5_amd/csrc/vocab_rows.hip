@@ -549,13 +549,13 @@ struct Geometry {
 };
 
 // Tuning knobs (trlx_set_tuning): 0 = automatic.
-static int g_row_variant = 0;       // 1 = register-resident rows, 2 = streaming rows
-static int g_resident_threads = 0;  // preferred workgroup size for resident rows
-static int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 6 waves/SIMD
-static int g_stream_threads = 0;
-static int g_stream_unroll = 0;
-static int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
-static int g_store_pol = 0;         // gradient-row stores: 0 auto, 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
+static thread_local int g_row_variant = 0;       // 1 = register-resident rows, 2 = streaming rows
+static thread_local int g_resident_threads = 0;  // preferred workgroup size for resident rows
+static thread_local int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 6 waves/SIMD
+static thread_local int g_stream_threads = 0;
+static thread_local int g_stream_unroll = 0;
+static thread_local int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
+static thread_local int g_store_pol = 0;         // gradient-row stores: 0 auto, 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
 constexpr double kSC1Bytes = 1.5e9;  // auto: sc1 above this many gradient bytes per launch, else nt
 
 // Cache policy of a launch's gradient-row stores (common.h store_grad_b128).  Measured
@@ -567,8 +567,8 @@ static int store_policy_for(double grad_bytes, bool split) {
     if (g_store_pol) return g_store_pol;
     return (!split && grad_bytes > kSC1Bytes) ? kStoreSC1 : kStoreNT;
 }
-static int g_split_lds = 0;         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
-static int g_split_mid = 0;         // mid bf16 rows (loss / backward): 0 auto (= 3), 1 off, 2 5+3, 3 6+2
+static thread_local int g_split_lds = 0;         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
+static thread_local int g_split_mid = 0;         // mid bf16 rows (loss / backward): 0 auto (= 3), 1 off, 2 5+3, 3 6+2
 int tuning_split_lds() { return g_split_lds; }
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
