@@ -86,9 +86,17 @@ def parse():
                    help="PPO: serial = PPOHotPath.step per batch; pipelined = pipeline_step (the next batch's "
                         "experience rows run while this batch's whitening all-reduce is in flight; bit-identical "
                         "results); auto = pipelined when N > 1 (there is no all-reduce at N = 1)")
+    p.add_argument("--dist", action="store_true",
+                   help="initialise the process group even at world size 1 (rehearses the RCCL path on one GPU: "
+                        "the whitening all-reduce then runs through RCCL every step)")
     p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
                         "several ranks on one GPU)")
+    p.add_argument("--comm", default="auto", choices=("auto", "rccl", "torch"),
+                   help="collectives of the PPO step under a process group: rccl = the boundary's RCCL helper "
+                        "(comm.RcclComm: ncclAllReduce enqueued on the step's stream, no ProcessGroupNCCL event "
+                        "joins); torch = torch.distributed.all_reduce; auto = rccl with the nccl backend, falling "
+                        "back to torch (reported in config.comm) if the communicator cannot be created")
     return p.parse_args()
 
 
@@ -328,14 +336,14 @@ def roofline(kern_ms, samples, ab, tokens, doms, elapsed, steps, traffic_key):
             "step_frac": round(ab["step"] * tokens / (elapsed / steps) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1):
+def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1, comm=None):
     x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
     cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
     ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
     pipelined = args.schedule == "pipelined" or (args.schedule == "auto" and world > 1)
     defer = not (pipelined or args.overlap_tail or args.no_defer_tail)
     hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=args.overlap_tail,
-                      loss_norm=args.loss_norm, defer_tail=defer)
+                      loss_norm=args.loss_norm, defer_tail=defer, comm=comm)
     fn = hp.pipeline_step if pipelined else hp.step  # pipelined: each call = E rows of one batch + loss of the last
 
     def step():
@@ -362,11 +370,24 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        kw = dict(rank=rank, world_size=world)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, **kw)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **kw)
+    comm, comm_kind = None, ("torch" if use_dist else None)
+    if use_dist and args.backend == "nccl" and args.comm != "torch" and args.config != "c5":
+        try:
+            comm = P.RcclComm.from_process_group(device=dev)
+            comm_kind = "rccl"
+        except Exception as e:  # auto: keep torch.distributed; rccl: explicit request, fail loudly
+            if args.comm == "rccl":
+                raise
+            print(f"warning: RCCL helper unavailable ({e}); using torch.distributed collectives", file=sys.stderr)
 
     B, T, V, desc = CONFIGS[args.config]
     if args.global_batch:
@@ -393,7 +414,7 @@ def main():
         schedule = "serial"
     else:
         ldt = torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16
-        hp, step, x = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world)
+        hp, step, x = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world, comm)
         schedule = "pipelined" if args.schedule == "pipelined" or (args.schedule == "auto" and world > 1) else "serial"
         names = {"experience", "loss"}
         tokens = B * T
@@ -413,7 +434,7 @@ def main():
             and not args.global_batch):
         del hp, step, x
         torch.cuda.empty_cache()
-        hp32, step32, x32 = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, torch.float32)
+        hp32, step32, x32 = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, torch.float32, world, comm)
         w32, wms32 = settle_and_warm(step32, torch, args, dev)
         el32, km32, sm32 = timed_run(step32, hp32, torch, dist, args, dev, world, names)
         fp32_line = {"value": round(tokens * args.steps / el32, 1), "unit": "tokens/s",
@@ -455,15 +476,18 @@ def main():
             "data": "synthetic",
             "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world, "seq_len": T, "vocab": V,
                        "logits_dtype": "fp32" if ilql else args.logits_dtype, "tokens_per_gpu_step": tokens,
-                       "parallelism": f"dp{world}", "schedule": schedule},
+                       "parallelism": f"dp{world}", "schedule": schedule, "comm": comm_kind},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         if fp32_line:
             out["fp32_logits"] = fp32_line
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
+        if comm is not None:
+            torch.cuda.synchronize(dev)
+            comm.close()
         dist.destroy_process_group()
     return out
 

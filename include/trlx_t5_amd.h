@@ -419,6 +419,25 @@ int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int
                                   const double* tail_stats, float vf_coef, float* loss, float* loss_stats,
                                   void* workspace, const trlx_kl_ctl* kl, void* stream);
 
+/* ---------------------------------------------------------------- RCCL stats all-reduce helper
+ * SURVEY §8b "Collectives" — replaces the two dist.all_reduce calls of
+ * get_global_statistics (trlx/utils/modeling.py:13-14, 18-19) on the hot path: ONE
+ * communicator per process, SUM of a small fp64 vector ({Σx, Σx², n[, Σmask]} or the score
+ * moments) enqueued on the caller's HIP stream — no side stream, no system-scope event join
+ * (each of ProcessGroupNCCL's costs ~20 us of compute-queue idle on MI355X).
+ *   trlx_comm_load      dlopen the RCCL the process already uses (PyTorch's librccl.so path)
+ *   trlx_comm_unique_id rank 0: ncclGetUniqueId into a trlx_comm_unique_id_bytes() buffer,
+ *                       which the caller broadcasts (the bindings use torch.distributed)
+ *   trlx_comm_init      every rank, collectively: ncclCommInitRank on the current HIP device
+ *   trlx_comm_allreduce_sum_f64   in-place SUM of buf[0:n] on `stream`
+ *   trlx_comm_destroy   ncclCommDestroy */
+int trlx_comm_load(const char* librccl_path);
+int64_t trlx_comm_unique_id_bytes(void);
+int trlx_comm_unique_id(void* id_out, int64_t nbytes);
+int trlx_comm_init(void** comm_out, const void* id, int64_t nbytes, int nranks, int rank);
+int trlx_comm_allreduce_sum_f64(void* comm, double* buf, int64_t n, void* stream);
+int trlx_comm_destroy(void* comm);
+
 /* ---------------------------------------------------------------- autograd plumbing
  * out[i] = x[i] * (*scale) for i < n (scale: device fp32 scalar, e.g. a backward's
  * grad_output).  In place (out == x) it is skipped entirely when *scale == 1. */

@@ -154,3 +154,60 @@ def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap):
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def rccl_world1_worker(port, inputs, xs_all, q):
+    """torch.distributed with the "nccl" backend (= RCCL on ROCm) at world size 1, on cuda:0:
+    the product's exchange path for real — ProcessGroupNCCL init with device_id, the async
+    whitening all-reduce + stream wait of pipeline_step, the blocking one of step(), and the
+    drop-in get_global_statistics / whiten / RunningMoments."""
+    import torch.distributed as dist
+    import trlx_t5_amd as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    x = {k: (v.to(dev) if v is not None else None) for k, v in inputs[0].items()}
+    B, T, V = x["logits"].shape
+    res = {"backend": dist.get_backend()}
+    comm = P.RcclComm.from_process_group(device=dev)
+    v = torch.randn(5, dtype=torch.float64, device=dev)
+    w = comm.allreduce_(v.clone())
+    torch.cuda.synchronize()
+    res["comm_identity"] = bool(torch.equal(v, w))
+    try:
+        comm.allreduce_(v.float())
+        res["comm_rejects_f32"] = False
+    except ValueError:
+        res["comm_rejects_f32"] = True
+    for mode, kind in (("serial", "torch"), ("pipelined", "torch"), ("serial", "rccl"), ("pipelined", "rccl")):
+        cfg = P.PPOConfig()
+        ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B)
+        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl,
+                          comm=comm if kind == "rccl" else None)
+        outs = []
+        for b in inputs:
+            xb = {k: (v.to(dev) if v is not None else None) for k, v in b.items()}
+            args = (xb["logits"], xb["ref_logits"], xb["new_logits"], xb["labels"], xb["old_values"], xb["values"],
+                    xb["scores"])
+            o = hp.step(*args) if mode == "serial" else hp.pipeline_step(*args)
+            if o is not None:
+                torch.cuda.synchronize()
+                outs.append([t.float().cpu().numpy() for t in o])
+        if mode == "pipelined":
+            o = hp.pipeline_flush()
+            torch.cuda.synchronize()
+            outs.append([t.float().cpu().numpy() for t in o])
+        torch.cuda.synchronize()
+        res[(mode, kind)] = (outs, hp.adv_stats.cpu().numpy(), ctl.state.cpu().numpy())
+    comm.close()
+    surf = {}
+    for key, xs in xs_all.items():
+        xd = xs.to(dev)
+        mean, var, count = P.get_global_statistics(xd)
+        surf[key] = (float(mean), float(var), float(count), P.whiten(xd).float().cpu().numpy(),
+                     P.whiten(xd, shift_mean=False).float().cpu().numpy())
+    res["surface"] = surf
+    q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()

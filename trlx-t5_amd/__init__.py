@@ -29,6 +29,7 @@ from .rollout_store import PPORLBatch, PPORLElement, PPORolloutStorage
 from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig, ILQLHotPath, ilql_sample_step
 from .control import PPOControlState
 from .step import PPOHotPath
+from .comm import RcclComm
 
 __all__ = [
     "logprobs_from_logits", "whiten", "get_global_statistics", "RunningMoments", "flatten_dict", "moments",
@@ -36,6 +37,7 @@ __all__ = [
     "prepare_scores", "stats_dict", "STATS_KEYS", "PPOHotPath", "load_library",
     "ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS", "ilql_sample_step", "PPORolloutStorage",
     "PPORLElement", "PPORLBatch", "lm_head_logprobs", "PPOControlState",
+    "RcclComm",
 ]
 
 

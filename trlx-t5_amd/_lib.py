@@ -124,6 +124,12 @@ SIGNATURES = {
                                           _score_ctl_p, _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                           _c_vp]),
     "trlx_ppo_rollout_loss_ctl": (_c_int, [_c_i64, _c_i64, _c_vp, _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
+    "trlx_comm_load": (_c_int, [ctypes.c_char_p]),
+    "trlx_comm_unique_id_bytes": (_c_i64, []),
+    "trlx_comm_unique_id": (_c_int, [_c_vp, _c_i64]),
+    "trlx_comm_init": (_c_int, [ctypes.POINTER(ctypes.c_void_p), _c_vp, _c_i64, _c_int, _c_int]),
+    "trlx_comm_allreduce_sum_f64": (_c_int, [_c_vp, _c_vp, _c_i64, _c_vp]),
+    "trlx_comm_destroy": (_c_int, [_c_vp]),
     "trlx_lsm_gather_fwd_loss_tail": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
                                                _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_vp, _c_f,
                                                _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),

@@ -36,17 +36,40 @@ from . import _lib
 from .modeling import grad_buffer_like
 from .control import PPOControlState
 from .ppo import PPOConfig
+from .comm import RcclComm
 from .timing import LaunchEvent, make_event
 
 __all__ = ["PPOHotPath"]
+
+
+class _StreamJoin:
+    """A pending side-stream all-reduce: wait() orders the current stream after it (a no-op
+    for one enqueued on the step's own stream).  Mirrors the torch Work.wait() the hot path
+    calls for torch.distributed collectives."""
+
+    __slots__ = ("_ev", "_dev")
+
+    def __init__(self, ev, device):
+        self._ev, self._dev = ev, device
+
+    def wait(self):
+        if self._ev is not None:
+            self._ev.wait(torch.cuda.current_stream(self._dev))
 
 
 class PPOHotPath:
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
                  device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
                  ctl: Optional[PPOControlState] = None, overlap_tail: bool = False, loss_norm: str = "rank",
-                 defer_tail: bool = False):
+                 defer_tail: bool = False, comm: Optional[RcclComm] = None):
         self.cfg = cfg
+        # comm: the boundary's RCCL helper (comm.RcclComm) for the step's all-reduces instead
+        # of torch.distributed — enqueued on the step's stream (blocking schedule) or on a side
+        # stream joined with fence-free events (pipelined schedule, score moments)
+        self.comm = comm
+        self._comm_stream = None
+        self._comm_events = [LaunchEvent() for _ in range(8)] if comm is not None else None
+        self._comm_ev_i = 0
         # defer_tail: the loss tail of step k runs as the first workgroups of step k+1's
         # experience rows launch (trlx_lsm_gather_fwd_loss_tail) instead of its own launch on
         # the critical path; loss / stats / beta of the last step are final after wait_stats()
@@ -157,6 +180,36 @@ class PPOHotPath:
                              f"{self.device} (got {t.dtype}, contiguous={t.is_contiguous()}, {t.device})")
         return t
 
+    # -------------------------------------------------------------- collectives
+    def _begin_step(self, scores, group, s):
+        """Whether the step is distributed, and the score moments all-reduce (device controller
+        state under DP) issued so it overlaps the experience rows: (global moments, work)."""
+        self.distributed = self.comm is not None or (dist.is_available() and dist.is_initialized())
+        if self.ctl is None:
+            return None, None
+        if self.comm is None:
+            return self.ctl._global_moments(scores, group, async_op=True)
+        _lib.call("trlx_score_moments", scores.data_ptr(), _lib.F32, scores.numel(), self.ctl.moments.data_ptr(),
+                  s.cuda_stream)
+        return self.ctl.moments, self._side_allreduce(self.ctl.moments[:3], s)
+
+    def _comm_event(self):
+        ev = self._comm_events[self._comm_ev_i]
+        self._comm_ev_i = (self._comm_ev_i + 1) % len(self._comm_events)
+        return ev
+
+    def _side_allreduce(self, t, s):
+        """comm.allreduce_(t) on a side stream after what `s` has queued; the returned handle's
+        wait() orders the then-current stream after it (fence-free events)."""
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(self.device)
+        ev_in, ev_out = self._comm_event(), self._comm_event()
+        ev_in.record(s)
+        ev_in.wait(self._comm_stream)
+        self.comm.allreduce_(t, self._comm_stream)
+        ev_out.record(self._comm_stream)
+        return _StreamJoin(ev_out, self.device)
+
     def _rollout_inputs(self, labels, lengths, mask, old_values, scores):
         B, T = self.B, self.T
         return (self._int64(labels, (B, T), "labels"), self._int64(lengths, (B,), "lengths", required=False),
@@ -173,10 +226,7 @@ class PPOHotPath:
         B, T, V = self.B, self.T, self.V
         labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
         s = torch.cuda.current_stream(self.device)
-        self.distributed = dist.is_available() and dist.is_initialized()
-        g_mom, work = None, None
-        if self.ctl is not None:  # score moments all-reduce overlaps the logits pass
-            g_mom, work = self.ctl._global_moments(scores, group, async_op=True)
+        g_mom, work = self._begin_step(scores, group, s)
         self._experience_rows(logits, ref_logits, labels, s)
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
         return self.lp_old, self.ref_lp
@@ -250,10 +300,7 @@ class PPOHotPath:
                                    lengths=lengths, mask=mask, group=group)
         s = torch.cuda.current_stream(self.device)
         self._launch_pending_tail(s)
-        self.distributed = dist.is_available() and dist.is_initialized()
-        g_mom, work = None, None
-        if self.ctl is not None:
-            g_mom, work = self.ctl._global_moments(scores, group, async_op=True)
+        g_mom, work = self._begin_step(scores, group, s)
         N = B * T
         nbytes = _lib.query("trlx_lmhead_workspace_bytes", N, V)
         if self.lm_ws is None or self.lm_ws.numel() < nbytes:
@@ -293,7 +340,14 @@ class PPOHotPath:
             # {Σ A, Σ A², n} (+ Σmask for the global loss normaliser): the only data-path exchange
             k = 4 if self.loss_norm == "global" else 3
             self._ar_group = group
-            self._ar_work = dist.all_reduce(self.adv_stats[:k], dist.ReduceOp.SUM, group=group, async_op=True)
+            if self.comm is not None:
+                if defer_allreduce:
+                    self._ar_work = self._side_allreduce(self.adv_stats[:k], s)
+                else:  # on the step's own stream: ordered with no join at all
+                    self.comm.allreduce_(self.adv_stats[:k], s)
+                    self._ar_work = _StreamJoin(None, self.device)
+            else:
+                self._ar_work = dist.all_reduce(self.adv_stats[:k], dist.ReduceOp.SUM, group=group, async_op=True)
             if not defer_allreduce:
                 self._resolve_allreduce()
 
@@ -305,7 +359,8 @@ class PPOHotPath:
             return
         w.wait()
         if self.loss_norm == "global":
-            self.adv_stats[3:4].div_(dist.get_world_size(self._ar_group))
+            world = self.comm.nranks if self.comm is not None else dist.get_world_size(self._ar_group)
+            self.adv_stats[3:4].div_(world)
 
     # -------------------------------------------------------------- K2
     def policy_loss(self, new_logits, labels, values, old_values, mask=None):
@@ -408,10 +463,7 @@ class PPOHotPath:
         prev = self._pending
         nb = self._pb ^ 1 if prev is not None else self._pb
         s = torch.cuda.current_stream(self.device)
-        self.distributed = dist.is_available() and dist.is_initialized()
-        g_mom, work = None, None
-        if self.ctl is not None:
-            g_mom, work = self.ctl._global_moments(scores, group, async_op=True)
+        g_mom, work = self._begin_step(scores, group, s)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
         self._experience_rows(logits, ref_logits, labels, s)
         out = self._pending_loss(s)
