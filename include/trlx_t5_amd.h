@@ -335,6 +335,15 @@ int trlx_rows_copy(int nfields, const void* const* src, void* const* dst, const 
                    const int64_t* cols, const int* esize, int64_t rows, const int64_t* src_idx,
                    int64_t src_row0, const int64_t* dst_idx, int64_t dst_row0, void* stream);
 
+/* decoder_input_ids of the seq2seq policy forward from a collated response batch — replaces
+ * shift_tokens_right (trlx/model/accelerate_ppo_model.py:18-25) as called by
+ * AcceleratePPOModel.get_model_inputs (:63-76): out[b,0] = decoder_start_token_id,
+ * out[b,t] = ids[b,t-1], then every -100 -> pad_token_id.  ids / out: device int64 [B, T] with
+ * row strides ld / out_ld (unit column stride), out must not alias ids; T >= 1 (the reference
+ * raises IndexError on an empty response), B = 0 is a no-op. */
+int trlx_shift_tokens_right(const int64_t* ids, int64_t B, int64_t T, int64_t ld, int64_t pad_token_id,
+                            int64_t decoder_start_token_id, int64_t* out, int64_t out_ld, void* stream);
+
 /* ---------------------------------------------------------------- §8f rank 4: device-resident controller state
  * The PPO loop's host scalars — RunningMoments of the scores (trlx/utils/modeling.py:72-104),
  * the orchestrator's ref_mean/ref_std + score scale/clip (ppo_orchestrator.py:48-49,96-112)

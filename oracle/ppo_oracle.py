@@ -287,3 +287,20 @@ def topk_mask(xs, k):
         return xs
     mintop = torch.topk(xs, k)[0][:, -1].unsqueeze(-1)
     return torch.where(xs < mintop, -np.inf * torch.ones_like(xs, dtype=xs.dtype), xs)
+
+
+# ------------------------------------------------------------------ accelerate_ppo_model.py:18-25,63-76
+def shift_tokens_right(ids, pad_token_id=0, decoder_start_token_id=0):
+    """Decoder inputs of the seq2seq forward: the start id, then the ids moved one column right;
+    every -100 (the start id included) becomes pad_token_id.  Empty responses (T = 0) raise
+    IndexError like the reference's column-0 assignment."""
+    if ids.dim() != 2 or ids.shape[1] == 0:
+        raise IndexError("shift_tokens_right needs [B, T >= 1] ids")
+    first = torch.full((ids.shape[0], 1), decoder_start_token_id, dtype=ids.dtype)
+    out = torch.cat([first, ids[:, :-1]], dim=1)
+    return torch.where(out == -100, torch.full_like(out, pad_token_id), out)
+
+
+def get_model_inputs(query_tensors, response_tensors):
+    """(encoder input, labels, decoder inputs) of AcceleratePPOModel.get_model_inputs."""
+    return query_tensors, response_tensors, shift_tokens_right(response_tensors)

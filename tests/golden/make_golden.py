@@ -19,6 +19,7 @@ Reference functions exercised (all file:line into /root/reference):
       imports ray, so its arithmetic is evaluated here with the reference's own ops,
       line for line, on the reference logprobs)
   trlx/model/nn/ilql_models.py:52-116  ILQLConfig.loss        (+ autograd grads)
+  trlx/model/accelerate_ppo_model.py:18-25,63-76  shift_tokens_right / get_model_inputs
 
 Run:  python tests/golden/make_golden.py      (writes tests/golden/*.npz)
 """
@@ -476,6 +477,52 @@ def make_topk(ilql_models):
     np.savez_compressed(os.path.join(OUT, "topk_mask.npz"), **out)
 
 
+# --------------------------------------------------------------------------- A9 model inputs
+def load_ppo_model_glue():
+    """trlx/model/accelerate_ppo_model.py for its module-level shift_tokens_right and the
+    self-free get_model_inputs.  Its import-time base classes live in files that import ray /
+    wandb / accelerate at module scope, so trlx.model and trlx.model.accelerate_base_model are
+    registered as shells carrying the two names the file binds (register_model: identity
+    decorator; AccelerateRLModel: an empty class) — nothing of them runs in the functions used."""
+    load_ppo_pipeline()
+    _load("trlx.data.configs", "trlx/data/configs.py")
+    m = _shell("trlx.model")
+    m.register_model = lambda c: c
+    b = _shell("trlx.model.accelerate_base_model")
+    b.AccelerateRLModel = type("AccelerateRLModel", (), {})
+    if "trlx.model.nn.ppo_models" not in sys.modules:
+        _shell("trlx.model.nn")
+        _load("trlx.model.nn.ppo_models", "trlx/model/nn/ppo_models.py")
+    return _load("trlx.model.accelerate_ppo_model", "trlx/model/accelerate_ppo_model.py")
+
+
+def make_model_inputs(apm):
+    """shift_tokens_right (:18-25) with its defaults and with explicit pad / start ids, -100
+    label ids (the start id -100 too), a width-1 response; get_model_inputs (:63-76)."""
+    out = {}
+    g = gen(900)
+    cases = {
+        "plain": (torch.randint(1, 32128, (5, 9), generator=g), {}),
+        "ignore": (torch.randint(-2, 50, (4, 12), generator=g), dict(pad_token_id=3, decoder_start_token_id=7)),
+        "start_ignored": (torch.randint(0, 9, (3, 6), generator=g), dict(pad_token_id=5, decoder_start_token_id=-100)),
+        "width1": (torch.randint(1, 100, (6, 1), generator=g), dict(decoder_start_token_id=2)),
+    }
+    cases["ignore"][0][cases["ignore"][0] < 0] = -100
+    cases["start_ignored"][0][:, ::2] = -100
+    for name, (ids, kw) in cases.items():
+        out[f"{name}/ids"] = ids.numpy()
+        out[f"{name}/pad"] = np.array(kw.get("pad_token_id", 0))
+        out[f"{name}/start"] = np.array(kw.get("decoder_start_token_id", 0))
+        out[f"{name}/out"] = apm.shift_tokens_right(ids.clone(), **kw).numpy()
+    q = torch.randint(0, 32128, (4, 7), generator=g)
+    r = torch.randint(0, 32128, (4, 5), generator=g)
+    r[1, 3:] = -100
+    a, b, c = apm.AcceleratePPOModel.get_model_inputs(None, q, r)
+    out["gmi/query"], out["gmi/response"] = q.numpy(), r.numpy()
+    out["gmi/input_seq"], out["gmi/labels"], out["gmi/decoder_input_ids"] = a.numpy(), b.numpy(), c.numpy()
+    np.savez_compressed(os.path.join(OUT, "model_inputs.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(4)
     only = sys.argv[1:]
@@ -498,6 +545,8 @@ if __name__ == "__main__":
         make_topk(ilql_models)
     if not only or "store" in only:
         make_rollout_store(*load_ppo_pipeline())
+    if not only or "inputs" in only:
+        make_model_inputs(load_ppo_model_glue())
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

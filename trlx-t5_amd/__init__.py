@@ -30,6 +30,7 @@ from .ilql import ILQL_LOSS_KEYS, ILQLBatch, ILQLConfig, ILQLHotPath, ilql_sampl
 from .control import PPOControlState
 from .step import PPOHotPath
 from .comm import RcclComm
+from .model_inputs import get_model_inputs, shift_tokens_right
 
 __all__ = [
     "logprobs_from_logits", "whiten", "get_global_statistics", "RunningMoments", "flatten_dict", "moments",
@@ -37,7 +38,7 @@ __all__ = [
     "prepare_scores", "stats_dict", "STATS_KEYS", "PPOHotPath", "load_library",
     "ILQLConfig", "ILQLBatch", "ILQLHotPath", "ILQL_LOSS_KEYS", "ilql_sample_step", "PPORolloutStorage",
     "PPORLElement", "PPORLBatch", "lm_head_logprobs", "PPOControlState",
-    "RcclComm",
+    "RcclComm", "shift_tokens_right", "get_model_inputs",
 ]
 
 

@@ -116,6 +116,7 @@ SIGNATURES = {
                                   _c_i64, _c_i64, _c_f, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_rows_copy": (_c_int, [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp,
                                 _c_i64, _c_vp, _c_i64, _c_vp]),
+    "trlx_shift_tokens_right": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp]),
     "trlx_ctl_init": (_c_int, [_c_vp, _c_d, _c_d, _c_d, _c_int, _c_vp]),
     "trlx_score_moments": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
     "trlx_score_ctl_update": (_c_int, [_c_vp, _c_int, _c_i64, _score_ctl_p, _c_vp, _c_int, _c_vp]),

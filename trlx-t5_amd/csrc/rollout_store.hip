@@ -66,9 +66,38 @@ __global__ __launch_bounds__(kRowsThreads) void k_rows_copy(RowsCopyArgs a) {
         copy_row<uint16_t>(f, sr, dr, lane);
 }
 
+// decoder_input_ids from the response tokens (shift_tokens_right, accelerate_ppo_model.py:18-25):
+//   out[b, 0] = start, out[b, t] = ids[b, t-1] (t >= 1), then every -100 (the label ignore id,
+//   the start id included) -> pad.  One thread per element, int64 in and out.
+__global__ __launch_bounds__(kRowsThreads) void k_shift_tokens_right(const int64_t* ids, int64_t B, int64_t T,
+                                                                    int64_t ld, int64_t pad, int64_t start,
+                                                                    int64_t* out, int64_t out_ld) {
+    const int64_t i = int64_t(blockIdx.x) * kRowsThreads + threadIdx.x;
+    if (i >= B * T) return;
+    const int64_t b = i / T, t = i - b * T;
+    const int64_t v = t == 0 ? start : ids[b * ld + t - 1];
+    out[b * out_ld + t] = v == -100 ? pad : v;
+}
+
 }  // namespace trlx
 
 using namespace trlx;
+
+extern "C" int trlx_shift_tokens_right(const int64_t* ids, int64_t B, int64_t T, int64_t ld,
+                                       int64_t pad_token_id, int64_t decoder_start_token_id, int64_t* out,
+                                       int64_t out_ld, void* stream) {
+    TRLX_REQUIRE(B >= 0 && T >= 1 && ld >= T && out_ld >= T, TRLX_ERR_SHAPE,
+                 "shift_tokens_right: bad shape B=%lld T=%lld (T >= 1, row strides >= T)", (long long)B,
+                 (long long)T);
+    TRLX_REQUIRE(B * T < (int64_t(1) << 31) * kRowsThreads, TRLX_ERR_SHAPE, "shift_tokens_right: too many tokens");
+    if (B == 0) return TRLX_OK;
+    TRLX_REQUIRE(ids && out, TRLX_ERR_ARG, "NULL argument to trlx_shift_tokens_right");
+    TRLX_REQUIRE(ids != out, TRLX_ERR_ARG, "shift_tokens_right: in-place call (out aliases ids)");
+    const unsigned grid = unsigned((B * T + kRowsThreads - 1) / kRowsThreads);
+    hipLaunchKernelGGL(k_shift_tokens_right, dim3(grid), dim3(kRowsThreads), 0, (hipStream_t)stream, ids, B, T,
+                       ld, pad_token_id, decoder_start_token_id, out, out_ld);
+    return check_launch("k_shift_tokens_right");
+}
 
 extern "C" int trlx_rows_copy(int nfields, const void* const* src, void* const* dst, const int64_t* src_ld,
                               const int64_t* dst_ld, const int64_t* src_col0, const int64_t* dst_col0,
