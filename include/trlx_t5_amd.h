@@ -396,6 +396,12 @@ int trlx_ctl_init(double* state, double init_kl_coef, double ref_mean, double re
 /* {Σx, Σx², n, 0} of scores (fp64, one workgroup) — the record a caller all-reduces across
  * ranks before trlx_score_ctl_update / trlx_ppo_rollout_gae_ctl. */
 int trlx_score_moments(const void* scores, int dtype, int64_t n, double* moments, void* stream);
+/* trlx_score_moments with `done_event` (a hipEvent_t) recorded by the kernel's own dispatch
+ * (hipExtLaunchKernel stop event) instead of a separate hipEventRecord marker between this
+ * launch and the next: the ordering point the RCCL helper's side stream waits on before the
+ * score-moments all-reduce. */
+int trlx_score_moments_signal(const void* scores, int dtype, int64_t n, double* moments, void* stream,
+                              void* done_event);
 /* One workgroup: the score-side control above; scores_out (may alias scores) receives the
  * scaled, clipped scores.  ppo_orchestrator.py:96-112. */
 int trlx_score_ctl_update(const void* scores, int dtype, int64_t n, const trlx_score_ctl* ctl,

@@ -119,6 +119,7 @@ SIGNATURES = {
     "trlx_shift_tokens_right": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp]),
     "trlx_ctl_init": (_c_int, [_c_vp, _c_d, _c_d, _c_d, _c_int, _c_vp]),
     "trlx_score_moments": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_vp]),
+    "trlx_score_moments_signal": (_c_int, [_c_vp, _c_int, _c_i64, _c_vp, _c_vp, _c_vp]),
     "trlx_score_ctl_update": (_c_int, [_c_vp, _c_int, _c_i64, _score_ctl_p, _c_vp, _c_int, _c_vp]),
     "trlx_kl_ctl_update": (_c_int, [_kl_ctl_p, _c_vp, _c_vp]),
     "trlx_ppo_rollout_gae_ctl": (_c_int, [_c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,

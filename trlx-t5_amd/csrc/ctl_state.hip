@@ -3,6 +3,8 @@
 // (RunningMoments.update + scale + clip, ppo_orchestrator.py:96-112) and the KL controller
 // update (ppo_models.py:26-58).  All are single-workgroup launches over small vectors; the
 // fused PPO step folds the same device code into its rollout tails (row_tails.h) instead.
+#include <hip/hip_ext.h>
+
 #include "ctl_state.h"
 
 namespace trlx {
@@ -70,6 +72,18 @@ extern "C" int trlx_score_moments(const void* scores, int dtype, int64_t n, doub
     TRLX_REQUIRE(scores && moments, TRLX_ERR_ARG, "NULL argument to trlx_score_moments");
     hipLaunchKernelGGL(k_score_moments, dim3(1), dim3(kCtlThreads), 0, (hipStream_t)stream,
                        static_cast<const float*>(scores), int(n), moments);
+    return check_launch("k_score_moments");
+}
+
+extern "C" int trlx_score_moments_signal(const void* scores, int dtype, int64_t n, double* moments, void* stream,
+                                         void* done_event) {
+    TRLX_REQUIRE(n > 0 && n < (1LL << 31), TRLX_ERR_SHAPE, "bad score count %lld", (long long)n);
+    TRLX_REQUIRE(dtype == TRLX_F32, TRLX_ERR_DTYPE, "scores must be fp32");
+    TRLX_REQUIRE(scores && moments && done_event, TRLX_ERR_ARG, "NULL argument to trlx_score_moments_signal");
+    // the event rides the kernel's own dispatch (its completion signal): no marker packet
+    // between this launch and the next one on the stream
+    hipExtLaunchKernelGGL(k_score_moments, dim3(1), dim3(kCtlThreads), 0, (hipStream_t)stream, nullptr,
+                          (hipEvent_t)done_event, 0, static_cast<const float*>(scores), int(n), moments);
     return check_launch("k_score_moments");
 }
 

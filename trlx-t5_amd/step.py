@@ -47,17 +47,22 @@ class _StreamJoin:
     for one enqueued on the step's own stream).  Mirrors the torch Work.wait() the hot path
     calls for torch.distributed collectives."""
 
-    __slots__ = ("_ev", "_dev")
+    __slots__ = ("_ev", "_dev", "_joined")
 
     def __init__(self, ev, device):
-        self._ev, self._dev = ev, device
+        self._ev, self._dev, self._joined = ev, device, None
 
     def wait(self):
-        if self._ev is not None:
-            self._ev.wait(torch.cuda.current_stream(self._dev))
+        # a stream wait is a barrier packet that idles the queue ~5 us even when already
+        # satisfied: a stream that has joined once is ordered after it for good
+        s = torch.cuda.current_stream(self._dev)
+        if self._ev is not None and self._joined != s.cuda_stream:
+            self._ev.wait(s)
+            self._joined = s.cuda_stream
 
 
 class PPOHotPath:
+    _comm_timing_events = False  # A/B knob: timing-capable events for the comm joins
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
                  device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
                  ctl: Optional[PPOControlState] = None, overlap_tail: bool = False, loss_norm: str = "rank",
@@ -68,8 +73,11 @@ class PPOHotPath:
         # stream joined with fence-free events (pipelined schedule, score moments)
         self.comm = comm
         self._comm_stream = None
-        self._comm_events = [LaunchEvent() for _ in range(8)] if comm is not None else None
+        self._comm_events = [LaunchEvent(timing=self._comm_timing_events) for _ in range(8)] \
+            if comm is not None else None
         self._comm_ev_i = 0
+        self._comm_inline = False
+        self._ar_unissued = None  # pipelined + comm: whitening record waiting for the next _begin_step
         # defer_tail: the loss tail of step k runs as the first workgroups of step k+1's
         # experience rows launch (trlx_lsm_gather_fwd_loss_tail) instead of its own launch on
         # the critical path; loss / stats / beta of the last step are final after wait_stats()
@@ -185,28 +193,51 @@ class PPOHotPath:
         """Whether the step is distributed, and the score moments all-reduce (device controller
         state under DP) issued so it overlaps the experience rows: (global moments, work)."""
         self.distributed = self.comm is not None or (dist.is_available() and dist.is_initialized())
-        if self.ctl is None:
-            return None, None
         if self.comm is None:
+            if self.ctl is None:
+                return None, None
             return self.ctl._global_moments(scores, group, async_op=True)
-        _lib.call("trlx_score_moments", scores.data_ptr(), _lib.F32, scores.numel(), self.ctl.moments.data_ptr(),
-                  s.cuda_stream)
-        return self.ctl.moments, self._side_allreduce(self.ctl.moments[:3], s)
+        # RCCL helper: the previous pipelined batch's whitening record (held back by
+        # _experience_tail) and these score moments share ONE side-stream segment and join
+        ts = [] if self._ar_unissued is None else [self._ar_unissued]
+        ready = None
+        if self.ctl is not None:
+            ready = None if self._comm_inline else self._comm_event()
+            if ready is None:
+                _lib.call("trlx_score_moments", scores.data_ptr(), _lib.F32, scores.numel(),
+                          self.ctl.moments.data_ptr(), s.cuda_stream)
+            else:  # the side stream's ordering point rides the moments kernel's dispatch
+                _lib.call("trlx_score_moments_signal", scores.data_ptr(), _lib.F32, scores.numel(),
+                          self.ctl.moments.data_ptr(), s.cuda_stream, ready.handle)
+            ts.append(self.ctl.moments[:3])
+        join = self._side_allreduce(ts, s, ready) if ts else None
+        if self._ar_unissued is not None:
+            self._ar_unissued, self._ar_work = None, join
+        return (self.ctl.moments, join) if self.ctl is not None else (None, None)
 
     def _comm_event(self):
         ev = self._comm_events[self._comm_ev_i]
         self._comm_ev_i = (self._comm_ev_i + 1) % len(self._comm_events)
         return ev
 
-    def _side_allreduce(self, t, s):
-        """comm.allreduce_(t) on a side stream after what `s` has queued; the returned handle's
-        wait() orders the then-current stream after it (fence-free events)."""
+    def _side_allreduce(self, ts, s, ready=None):
+        """comm.allreduce_ of each tensor in `ts` (each its own collective, the same sizes as
+        the blocking schedule's, so every element is summed in the same order) on a side
+        stream after what `s` has queued; the returned handle's wait() orders the then-current
+        stream after them (ordering-only fence-free events: one join per call)."""
+        if self._comm_inline:  # A/B only: on `s` itself (no overlap, no joins)
+            for t in ts:
+                self.comm.allreduce_(t, s)
+            return _StreamJoin(None, self.device)
         if self._comm_stream is None:
             self._comm_stream = torch.cuda.Stream(self.device)
-        ev_in, ev_out = self._comm_event(), self._comm_event()
-        ev_in.record(s)
+        ev_in, ev_out = ready, self._comm_event()
+        if ev_in is None:  # `ready`: already recorded on `s` by the last launch
+            ev_in = self._comm_event()
+            ev_in.record(s)
         ev_in.wait(self._comm_stream)
-        self.comm.allreduce_(t, self._comm_stream)
+        for t in ts:
+            self.comm.allreduce_(t, self._comm_stream)
         ev_out.record(self._comm_stream)
         return _StreamJoin(ev_out, self.device)
 
@@ -341,8 +372,8 @@ class PPOHotPath:
             k = 4 if self.loss_norm == "global" else 3
             self._ar_group = group
             if self.comm is not None:
-                if defer_allreduce:
-                    self._ar_work = self._side_allreduce(self.adv_stats[:k], s)
+                if defer_allreduce:  # issued with the next batch's score moments (_begin_step)
+                    self._ar_unissued, self._ar_work = self.adv_stats[:k], None
                 else:  # on the step's own stream: ordered with no join at all
                     self.comm.allreduce_(self.adv_stats[:k], s)
                     self._ar_work = _StreamJoin(None, self.device)
@@ -354,6 +385,9 @@ class PPOHotPath:
     def _resolve_allreduce(self):
         """Order the current stream after the pending whitening all-reduce (RCCL: a stream
         wait, no host sync) and finish the global loss normaliser."""
+        if self._ar_unissued is not None:  # the last pipelined batch: nothing left to hide it behind
+            self.comm.allreduce_(self._ar_unissued, torch.cuda.current_stream(self.device))
+            self._ar_unissued, self._ar_work = None, _StreamJoin(None, self.device)
         w, self._ar_work = self._ar_work, None
         if w is None:
             return

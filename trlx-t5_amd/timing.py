@@ -13,6 +13,7 @@ import os
 
 import torch  # noqa: F401  (loads the HIP runtime this module binds)
 
+_HIP_EVENT_DISABLE_TIMING = 0x2
 _HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000
 _hip = None
 
@@ -52,11 +53,17 @@ class LaunchEvent:
 
     __slots__ = ("_ev",)
 
-    def __init__(self):
+    def __init__(self, timing: bool = True):
+        """timing=False: an ordering-only event (hipEventDisableTiming; no timestamp write)."""
         ev = ctypes.c_void_p()
-        _check(_runtime().hipEventCreateWithFlags(ctypes.byref(ev), _HIP_EVENT_DISABLE_SYSTEM_FENCE),
-               "hipEventCreateWithFlags")
+        flags = _HIP_EVENT_DISABLE_SYSTEM_FENCE | (0 if timing else _HIP_EVENT_DISABLE_TIMING)
+        _check(_runtime().hipEventCreateWithFlags(ctypes.byref(ev), flags), "hipEventCreateWithFlags")
         self._ev = ev
+
+    @property
+    def handle(self):
+        """The raw hipEvent_t (for C-ABI entry points that record it with a launch)."""
+        return self._ev.value
 
     def record(self, stream):
         """stream: a torch.cuda.Stream (its raw hipStream_t is used)."""
