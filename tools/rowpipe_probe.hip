@@ -48,7 +48,7 @@ __device__ __forceinline__ float vmax(const vec4u* v) {
     return m;
 }
 
-template <int SPOL>
+template <int SPOL, int LAUX = kAuxNT>
 __global__ __launch_bounds__(THR, 4) void k_rowwg(const char* x, char* y, int R) {
     __shared__ float sh[THR / 64];
     const int64_t r = blockIdx.x;
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(THR, 4) void k_rowwg(const char* x, char* y, int R)
     const int voff = threadIdx.x * 16;
     vec4u v[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, launder_int(voff) + k * THR * 16, 0, kAuxNT);
+    for (int k = 0; k < NV; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(ri, launder_int(voff) + k * THR * 16, 0, LAUX);
     const float s = 1.0f / (1.0f + fabsf(probe_block_max(vmax(v), sh)));
 #pragma unroll
     for (int k = 0; k < NV; ++k) st<SPOL>(v[k], s, ro, launder_int(voff) + k * THR * 16);
@@ -124,12 +124,15 @@ int main() {
     CHECK(hipMemset(x, 0x3c, size_t(R) * kRowStride));
     const double bytes = 2.0 * R * double(kRowBytes);
     const int G = 512;
-    struct V { const char* name; float ms; } res[8];
+    struct V { const char* name; float ms; } res[12];
     int n = 0;
     for (int pass = 0; pass < 2; ++pass) {
         n = 0;
         res[n++] = {"rowwg nt", timeit([&] { hipLaunchKernelGGL((k_rowwg<kStoreNT>), dim3(R), dim3(THR), 0, 0, x, y, R); }, 10)};
         res[n++] = {"rowwg sc1", timeit([&] { hipLaunchKernelGGL((k_rowwg<kStoreSC1>), dim3(R), dim3(THR), 0, 0, x, y, R); }, 10)};
+        res[n++] = {"rowwg none", timeit([&] { hipLaunchKernelGGL((k_rowwg<kStoreNone>), dim3(R), dim3(THR), 0, 0, x, y, R); }, 10)};
+        res[n++] = {"rowwg nt ld-default", timeit([&] { hipLaunchKernelGGL((k_rowwg<kStoreNT, 0>), dim3(R), dim3(THR), 0, 0, x, y, R); }, 10)};
+        res[n++] = {"rowwg ntsc1", timeit([&] { hipLaunchKernelGGL((k_rowwg<kStoreNTSC1>), dim3(R), dim3(THR), 0, 0, x, y, R); }, 10)};
         res[n++] = {"persist nt", timeit([&] { hipLaunchKernelGGL((k_persist<kStoreNT, false>), dim3(G), dim3(THR), 0, 0, x, y, R); }, 10)};
         res[n++] = {"persist-il nt", timeit([&] { hipLaunchKernelGGL((k_persist<kStoreNT, true>), dim3(G), dim3(THR), 0, 0, x, y, R); }, 10)};
         res[n++] = {"persist-il sc1", timeit([&] { hipLaunchKernelGGL((k_persist<kStoreSC1, true>), dim3(G), dim3(THR), 0, 0, x, y, R); }, 10)};
