@@ -43,6 +43,30 @@ def test_library_exports_every_declared_symbol(built_lib):
     assert built_lib.trlx_abi_version() == _lib.ABI_VERSION
 
 
+@pytest.fixture(scope="module")
+def fresh_lib(tmp_path_factory):
+    """The library built from the sources at HEAD into a scratch dir (never the in-tree .so,
+    which may predate the sources): a tree that does not compile fails the CPU suite."""
+    d = tmp_path_factory.mktemp("fresh_build")
+    out = d / "libtrlx_t5_amd.so"
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "trlx-t5_amd", "csrc"), f"-j{min(8, os.cpu_count() or 1)}",
+                        f"OUT={out}", f"BUILD={d / 'obj'}"], capture_output=True, text=True)
+    assert r.returncode == 0, "HIP library does not build from source:\n" + r.stderr[-4000:]
+    return str(out)
+
+
+def test_fresh_build_exports_exactly_the_header(fresh_lib):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", fresh_lib]).decode()
+    exported = set(re.findall(r"\bT (trlx_\w+)", out))
+    declared = set(header_functions())
+    assert declared - exported == set(), f"declared but not exported: {declared - exported}"
+    assert exported - declared == set(), f"exported but not declared / bound: {exported - declared}"
+    assert b"gfx950" in open(fresh_lib, "rb").read()
+    in_tree = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH]).decode() \
+        if os.path.exists(_lib.LIB_PATH) else ""
+    assert set(re.findall(r"\bT (trlx_\w+)", in_tree)) == exported, "in-tree .so is stale: rebuild with make"
+
+
 def test_library_is_gfx950_code(built_lib):
     assert b"gfx950" in open(_lib.LIB_PATH, "rb").read()
 

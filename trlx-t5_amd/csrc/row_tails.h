@@ -29,8 +29,7 @@ __device__ __forceinline__ double wave_allsum_d(double v) {
 }
 
 // Workspace carve-up (16-B aligned sections), see trlx_ppo_workspace_bytes:
-//   tickets : uint32[4]                    (zero before first use; re-armed in-kernel):
-//             [0] GAE ticket, [1] loss-tail ticket, [2] folded-GAE ready flag (gae_block<true>)
+//   tickets : uint32[4]                    (zero before first use; re-armed in-kernel)
 //   gae_rec : double[nblk][4]              per-block moments
 //   loss_rec: double[nblk][16]             per-block loss sums
 //   tokrec  : float[B*T][kTokRec]          per-token loss terms
@@ -67,23 +66,10 @@ struct GaeRolloutArgs {
 // lane-parallel scan (log2 64 steps) per 64-token chunk from the end, the carry
 // A_{chunk end} entering with weight c^(n).  fp32 re-association vs the reference's
 // sequential loop: ~1e-7 relative.
-//
-// One block of kGaeThreads (8 rollouts, one wave each) = block `blk` of `nblk`.  The same
-// function runs as k_rollout_gae and as the first workgroups of the loss rows launch
-// (trlx_ppo_loss_rows_gae): the block size, and with it every reduction order, is the same
-// in both.  HANDOFF (folded): the loss rows of the same launch read adv / returns / the
-// moments, so those bytes are stored write-through (`sc1`: relaxed agent-scope atomic
-// stores) and drained before the block's ticket; the block that reduces the moments stores
-// them the same way and then raises ws.tickets[2] (MI355X_MICROARCH.md "Valid forms", table
-// row 1; the row workgroups poll it and read the bytes with `sc1` loads).  The loss tail
-// lowers the flag again (loss_tail_block), so it is 0 whenever a loss rows launch starts.
-constexpr int kGaeThreads = 512;
-constexpr int kGaeRolloutsPerBlock = kGaeThreads / kWave;
-
-template <bool HANDOFF>
-__device__ __forceinline__ void gae_block(const GaeRolloutArgs& e, int blk, int nblk, double* red) {
+__global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs e) {
+    __shared__ double red[kRolloutsPerBlock * TRLX_MOMENT_SLOTS];
     const int lane = threadIdx.x & (kWave - 1);
-    const int b = blk * int(blockDim.x / kWave) + int(threadIdx.x / kWave);
+    const int b = blockIdx.x * kRolloutsPerBlock + threadIdx.x / kWave;
     const int T = e.T;
     double s1 = 0.0, s2 = 0.0, sm = 0.0, cnt = 0.0;
     float neg_beta = e.neg_beta, sdiv = 0.0f, sclip = 0.0f;
@@ -94,7 +80,7 @@ __device__ __forceinline__ void gae_block(const GaeRolloutArgs& e, int blk, int 
     const bool ctl_first = e.has_ctl && e.ctl.scale_mode != TRLX_SCALE_NONE;
     if (ctl_first) {
         float beta;
-        score_ctl_block(e.ctl, e.scores, e.B, blk == 0, sdiv, beta);
+        score_ctl_block(e.ctl, e.scores, e.B, blockIdx.x == 0, sdiv, beta);
         neg_beta = -beta;
     } else if (e.has_ctl) {
         neg_beta = -float(e.ctl.state_in[TRLX_CTL_KL_COEF]);
@@ -130,14 +116,8 @@ __device__ __forceinline__ void gae_block(const GaeRolloutArgs& e, int blk, int 
             vcarry = __shfl(v, 0, kWave);
             if (ok) {
                 e.rewards[gi] = r;
-                if constexpr (HANDOFF) {  // ret is fp32 here (checked at launch)
-                    __hip_atomic_store(e.adv + gi, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(static_cast<float*>(e.ret) + gi, add_rn(A, v), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    e.adv[gi] = A;
-                    st_any(e.ret, e.ret_dtype, gi, add_rn(A, v));
-                }
+                e.adv[gi] = A;
+                st_any(e.ret, e.ret_dtype, gi, add_rn(A, v));
                 s1 += double(A);
                 s2 += double(A) * double(A);
                 sm += e.mask ? double(e.mask[gi]) : 1.0;
@@ -145,33 +125,18 @@ __device__ __forceinline__ void gae_block(const GaeRolloutArgs& e, int blk, int 
             }
         }
     }
-    if (e.has_ctl && !ctl_first && blk == 0) {
+    if (e.has_ctl && !ctl_first && blockIdx.x == 0) {
         float d_unused, b_unused;
         score_ctl_block(e.ctl, e.scores, e.B, true, d_unused, b_unused);
     }
-    if constexpr (HANDOFF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adv / ret stores
     const double mine[TRLX_MOMENT_SLOTS] = {s1, s2, cnt, sm};
     const double rec = block_sum_multi<TRLX_MOMENT_SLOTS>(mine, red);
-    if (publish_record_last<TRLX_MOMENT_SLOTS>(e.ws.gae_rec + blk * TRLX_MOMENT_SLOTS, rec, e.ws.tickets + 0,
-                                               unsigned(nblk))) {
+    if (publish_record_last<TRLX_MOMENT_SLOTS>(e.ws.gae_rec + blockIdx.x * TRLX_MOMENT_SLOTS, rec,
+                                               e.ws.tickets + 0, gridDim.x)) {
         __syncthreads();  // red[] reuse
-        const double tot = reduce_records<TRLX_MOMENT_SLOTS>(e.ws.gae_rec, nblk, red);
-        if constexpr (HANDOFF) {
-            if (threadIdx.x < TRLX_MOMENT_SLOTS) {
-                __hip_atomic_store(e.stats + threadIdx.x, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_store(e.ws.tickets + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (threadIdx.x < TRLX_MOMENT_SLOTS) e.stats[threadIdx.x] = tot;
-        }
+        const double tot = reduce_records<TRLX_MOMENT_SLOTS>(e.ws.gae_rec, gridDim.x, red);
+        if (threadIdx.x < TRLX_MOMENT_SLOTS) e.stats[threadIdx.x] = tot;
     }
-}
-
-__global__ __launch_bounds__(kGaeThreads) void k_rollout_gae(GaeRolloutArgs e) {
-    __shared__ double red[kGaeRolloutsPerBlock * TRLX_MOMENT_SLOTS];
-    gae_block<false>(e, int(blockIdx.x), int(gridDim.x), red);
 }
 
 // ------------------------------------------------------------------ loss sums per rollout
@@ -246,9 +211,6 @@ __device__ __forceinline__ void loss_token_terms(const LossTokenArgs& L, float* 
 __device__ __forceinline__ void loss_tail_block(const LossRolloutArgs& L, int blk, int nblk, double* red) {
     const int lane = threadIdx.x & (kWave - 1);
     const int b = blk * int(blockDim.x / kWave) + int(threadIdx.x / kWave);
-    // the loss rows launch this tail follows has read everything a folded GAE handed it:
-    // lower the hand-off flag for the next one (gae_block<true>)
-    if (blk == 0 && threadIdx.x == 0) __hip_atomic_store(L.ws.tickets + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     double acc[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc[k] = 0.0;

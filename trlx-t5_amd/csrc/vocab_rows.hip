@@ -53,16 +53,10 @@ struct RowArgs {
     // fused loss: per-token loss records + value gradient (row_tails.h)
     float* tokrec;
     LossTokenArgs ltok;
-    // Work folded into the launch as its first `lead_blocks` workgroups; row = blockIdx.x -
-    // lead_blocks.  Forward: the PREVIOUS step's loss tail (trlx_lsm_gather_fwd_loss_tail).
-    // Fused loss: this step's GAE tail (trlx_ppo_loss_rows_gae), whose adv / returns /
-    // moments the row workgroups wait for on `gae_ready` (gae_block<true>).
-    int lead_blocks;
-    int has_tail;
+    // forward only: the PREVIOUS step's loss tail folded into this launch as its first
+    // `tail_blocks` workgroups (trlx_lsm_gather_fwd_loss_tail); row = blockIdx.x - tail_blocks
+    int has_tail, tail_blocks;
     LossRolloutArgs tail;
-    int has_gae;
-    GaeRolloutArgs gae;
-    const unsigned* gae_ready;
 };
 
 // ------------------------------------------------------------------ shared row pieces
@@ -75,7 +69,7 @@ struct Row {
     bool y_ok;
     RowSplit<DT> s;
     __device__ __forceinline__ Row(const RowArgs& a)
-        : row(int64_t(blockIdx.x) - a.lead_blocks),
+        : row(int64_t(blockIdx.x) - a.tail_blocks),
           b(row / a.T),
           t(row - b * a.T),
           x(reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st),
@@ -107,32 +101,6 @@ __device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row)
     const double msum = a.msum ? *a.msum : a.msum_host;
     p.inv_msum = 1.0f / float(msum);  // torch: grad / mask.sum()
     p.olp = ld_any(a.old_lp, a.old_dtype, row);
-    return p;
-}
-
-// The same after a folded GAE (thread 0 of a row workgroup): wait for its ready flag, then
-// read what it handed over -- adv, the moments (whitening + Σmask) and the token's return --
-// with `sc1` loads (MI355X_MICROARCH.md "Valid forms", table row 1).  Issued after the row's
-// own loads, so a satisfied poll costs the row nothing; the first rows of the launch wait
-// here while the GAE workgroups run (their loads already in flight).
-__device__ __forceinline__ PpoScalars ppo_scalars_handoff(const RowArgs& a, int64_t row, float* ret_out) {
-    for (int spin = 0; spin < (1 << 22); ++spin) {  // bounded: a lost flag shows up as wrong numbers, not a hang
-        if (__hip_atomic_load(a.gae_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    PpoScalars p;
-    p.A = __hip_atomic_load(a.adv + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    double st[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) st[k] = __hip_atomic_load(a.stats + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    float mu, rstd;
-    whiten_coeffs(st, a.unbiased, mu, rstd);
-    p.A = mul_rn(p.A - mu, rstd);
-    p.m = a.mask ? float(a.mask[row]) : 1.0f;
-    p.inv_msum = 1.0f / float(st[3]);  // a.msum is stats + 3 here
-    p.olp = ld_any(a.old_lp, a.old_dtype, row);
-    *ret_out = __hip_atomic_load(static_cast<const float*>(a.ltok.returns) + row, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
     return p;
 }
 
@@ -179,16 +147,9 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     __shared__ float sh_max2[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     if constexpr (MODE == kFwd) {
-        if (int(blockIdx.x) < a.lead_blocks) {  // the previous step's loss tail (block-uniform branch)
+        if (int(blockIdx.x) < a.tail_blocks) {  // the previous step's loss tail (block-uniform branch)
             __shared__ double tail_red[kMaxThreads / kWave * 16];
-            if (blockIdx.y == 0) loss_tail_block(a.tail, int(blockIdx.x), a.lead_blocks, tail_red);
-            return;
-        }
-    }
-    if constexpr (MODE == kPpo) {
-        if (int(blockIdx.x) < a.lead_blocks) {  // this step's GAE tail (512-thread launches only)
-            __shared__ double gae_red[kGaeRolloutsPerBlock * TRLX_MOMENT_SLOTS];
-            gae_block<true>(a.gae, int(blockIdx.x), a.lead_blocks, gae_red);
+            if (blockIdx.y == 0) loss_tail_block(a.tail, int(blockIdx.x), a.tail_blocks, tail_red);
             return;
         }
     }
@@ -200,7 +161,7 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     // flight and parked in LDS (read back after the reductions' barriers): they then
     // occupy no VGPRs beside the row.
     __shared__ float s_ps[7];
-    if (MODE == kPpo && tid == 0 && !a.gae_ready) {
+    if (MODE == kPpo && tid == 0) {
         const PpoScalars p0 = ppo_scalars(a, r.row);
         s_ps[0] = p0.A; s_ps[1] = p0.m; s_ps[2] = p0.inv_msum; s_ps[3] = p0.olp;
         if (a.tokrec) loss_token_inputs(a.ltok, r.row, s_ps + 4);
@@ -234,16 +195,6 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
             const int ic = unsigned(i) < unsigned(nvec) ? i : 0;  // out-of-row lanes: any valid address
             __builtin_amdgcn_global_load_lds(body + int64_t(ic) * 16,
                                              (__attribute__((address_space(3))) void*)(lbase + kk * 8192), 16, 0, 0);
-        }
-    }
-    if (MODE == kPpo && tid == 0 && a.gae_ready) {  // folded GAE: its results, behind the row loads
-        float ret;
-        const PpoScalars p0 = ppo_scalars_handoff(a, r.row, &ret);
-        s_ps[0] = p0.A; s_ps[1] = p0.m; s_ps[2] = p0.inv_msum; s_ps[3] = p0.olp;
-        if (a.tokrec) {
-            s_ps[4] = ld_any(a.ltok.values, a.ltok.v_dtype, r.row);
-            s_ps[5] = ld_any(a.ltok.old_values, a.ltok.ov_dtype, r.row);
-            s_ps[6] = ret;
         }
     }
     const float xy = r.y_ok ? DT::load1(r.x, r.y) : NAN;
@@ -653,30 +604,17 @@ static bool rows_same_phase(const RowArgs& a, size_t es) {
     return same_steps && ((reinterpret_cast<uintptr_t>(a.x0) ^ reinterpret_cast<uintptr_t>(a.dx)) & 15u) == 0;
 }
 
-// Kernels that cannot host the folded GAE tail (the block size must be kGaeThreads: every
-// reduction order is the standalone kernel's) run it as its own launch first.
-static int gae_standalone(RowArgs& a, hipStream_t stream) {
-    if (!a.has_gae) return TRLX_OK;
-    a.has_gae = 0;
-    a.gae_ready = nullptr;
-    const unsigned nblk = unsigned((a.gae.B + kGaeRolloutsPerBlock - 1) / kGaeRolloutsPerBlock);
-    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kGaeThreads), 0, stream, a.gae);
-    return check_launch("k_rollout_gae");
-}
-
-// A folded loss tail needs one workgroup per (threads / 64) rollouts ahead of the rows; a
-// folded GAE tail one per kGaeRolloutsPerBlock rollouts (threads == kGaeThreads).
+// A folded loss tail needs one workgroup per (threads / 64) rollouts ahead of the rows.
 static dim3 rows_grid(RowArgs& a, int threads, int nten) {
-    a.lead_blocks = a.has_tail ? int((a.tail.B + threads / kWave - 1) / (threads / kWave)) : 0;
-    if (a.has_gae) a.lead_blocks = int((a.gae.B + kGaeRolloutsPerBlock - 1) / kGaeRolloutsPerBlock);
-    return dim3(unsigned(a.B * a.T + a.lead_blocks), unsigned(nten));
+    a.tail_blocks = a.has_tail ? int((a.tail.B + threads / kWave - 1) / (threads / kWave)) : 0;
+    return dim3(unsigned(a.B * a.T + a.tail_blocks), unsigned(nten));
 }
 
 // Kernels that cannot host the folded loss tail run it as its own launch first.
 static int tail_standalone(RowArgs& a, hipStream_t stream) {
     if (!a.has_tail) return TRLX_OK;
     a.has_tail = 0;
-    a.lead_blocks = 0;
+    a.tail_blocks = 0;
     const unsigned nblk = unsigned((a.tail.B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
     hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, stream, a.tail);
     return check_launch("k_rollout_loss");
@@ -736,9 +674,7 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
     if (variant == 2 || g.nv == 0) {
-        int rc = tail_standalone(a, stream);
-        if (rc) return rc;
-        rc = gae_standalone(a, stream);
+        const int rc = tail_standalone(a, stream);
         if (rc) return rc;
         const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
         const int thr = g_stream_threads ? g_stream_threads : kStreamMaxThreads;
@@ -752,10 +688,6 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
         return check_launch("k_vocab_rows_stream");
     }
     const dim3 block(g.threads);
-    if (g.threads != kGaeThreads) {
-        const int rc = gae_standalone(a, stream);
-        if (rc) return rc;
-    }
     const dim3 grid = rows_grid(a, g.threads, nten);
     const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
     const bool lb512 = g.threads <= 512 && g_resident_lb512;
@@ -893,16 +825,15 @@ extern "C" int64_t trlx_ppo_workspace_bytes(int64_t B, int64_t T) {
     return int64_t(carve_workspace(nullptr, B, T, nullptr));
 }
 
-static int fill_gae(GaeRolloutArgs* ep, int64_t B, int64_t T, const float* lp, const float* ref_lp,
-                    const void* values, int v_dtype, const float* scores, const int64_t* lengths,
-                    const int64_t* mask, float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam,
-                    float* rewards, float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace) {
+static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                            int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                            float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
+                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream) {
     TRLX_REQUIRE(B > 0 && T > 0 && B * T < (1LL << 31), TRLX_ERR_SHAPE, "bad rollout batch %lld x %lld",
                  (long long)B, (long long)T);
     TRLX_REQUIRE(lp && ref_lp && values && rewards && adv_raw && ret && stats && workspace, TRLX_ERR_ARG,
                  "NULL argument to trlx_ppo_rollout_gae");
-    GaeRolloutArgs& e = *ep;
-    e = {};
+    GaeRolloutArgs e = {};
     carve_workspace(workspace, B, T, &e.ws);
     e.B = int(B); e.T = int(T); e.lp = lp; e.ref_lp = ref_lp; e.values = values; e.v_dtype = v_dtype;
     e.scores = scores; e.lengths = lengths; e.mask = mask; e.neg_beta = -kl_coef; e.gamma = gamma;
@@ -919,224 +850,8 @@ static int fill_gae(GaeRolloutArgs* ep, int64_t B, int64_t T, const float* lp, c
         e.ctl.state_in = ctl->state_in; e.ctl.state_out = ctl->state_out; e.ctl.global_mom = ctl->global_moments;
         e.ctl.scale_mode = ctl->scale_mode; e.ctl.clip = ctl->cliprange_reward;
     }
-    return TRLX_OK;
-}
-
-static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
-                            int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
-                            float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
-                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream) {
-    GaeRolloutArgs e;
-    const int rc = fill_gae(&e, B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, ctl, gamma, lam,
-                            rewards, adv_raw, ret, ret_dtype, stats, workspace);
-    if (rc) return rc;
-    const unsigned nblk = unsigned((B + kGaeRolloutsPerBlock - 1) / kGaeRolloutsPerBlock);
-    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kGaeThreads), 0, (hipStream_t)stream, e);
-    return check_launch("k_rollout_gae");
-}
-
-extern "C" int trlx_ppo_rollout_gae(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
-                                    int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
-                                    float kl_coef, float gamma, float lam, float* rewards, float* adv_raw, void* ret,
-                                    int ret_dtype, double* stats, void* workspace, void* stream) {
-    return rollout_gae_impl(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, nullptr, gamma, lam,
-                            rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
-}
-
-extern "C" int trlx_ppo_rollout_gae_ctl(int64_t B, int64_t T, const float* lp, const float* ref_lp,
-                                        const void* values, int v_dtype, const float* scores,
-                                        const int64_t* lengths, const int64_t* mask, const trlx_score_ctl* ctl,
-                                        float gamma, float lam, float* rewards, float* adv_raw, void* ret,
-                                        int ret_dtype, double* stats, void* workspace, void* stream) {
-    TRLX_REQUIRE(ctl, TRLX_ERR_ARG, "NULL trlx_score_ctl");
-    return rollout_gae_impl(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, 0.0f, ctl, gamma, lam,
-                            rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
-}
-
-extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dtype, int64_t B,
-                                         int64_t T, int64_t V, int64_t sb, int64_t st, const int64_t* labels,
-                                         int64_t lb, int64_t lt, const void* values, int v_dtype,
-                                         const float* scores, const int64_t* lengths, const int64_t* mask,
-                                         float kl_coef, float gamma, float lam, float* lp, float* ref_lp,
-                                         float* rewards, float* adv_raw, void* ret, int ret_dtype,
-                                         double* stats, void* workspace, void* stream) {
-    TRLX_REQUIRE(ref_logits, TRLX_ERR_ARG, "NULL reference logits");
-    int rc = trlx_lsm_gather_fwd(logits, ref_logits, dtype, B, T, V, sb, st, labels, lb, lt, lp, ref_lp, TRLX_F32,
-                                 nullptr, nullptr, stream);
-    if (rc) return rc;
-    return trlx_ppo_rollout_gae(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, gamma, lam,
-                                rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
-}
-
-static int fill_loss_rows(RowArgs* ap, const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
-                          int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
-                          int old_dtype, const float* adv_raw, const double* stats, int unbiased,
-                          const int64_t* mask, const void* values, int v_dtype, const void* old_values,
-                          int ov_dtype, const void* returns, int r_dtype, float cliprange, float cliprange_value,
-                          float vf_coef, float* lp_out, void* dx, int64_t dsb, int64_t dst, float* dvalues,
-                          void* workspace) {
-    RowArgs& a = *ap;
-    a.x0 = logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
-    a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv_raw; a.stats = stats; a.unbiased = unbiased;
-    a.mask = mask; a.msum = stats ? stats + 3 : nullptr; a.msum_host = double(B * T); a.cliprange = cliprange;
-    a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
-    int rc = check_rows(a, dtype);
-    if (rc) return rc;
-    TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
-    TRLX_REQUIRE(old_lp && adv_raw && stats && values && old_values && returns && lp_out && dx && dvalues && workspace,
-                 TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_rows");
-    Workspace ws;
-    carve_workspace(workspace, B, T, &ws);
-    a.tokrec = ws.tokrec;
-    a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
-    a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
-    a.ltok.dv = dvalues;
-    return TRLX_OK;
-}
-
-extern "C" int trlx_ppo_loss_rows(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
-                                  int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
-                                  int old_dtype, const float* adv_raw, const double* stats, int unbiased,
-                                  const int64_t* mask, const void* values, int v_dtype, const void* old_values,
-                                  int ov_dtype, const void* returns, int r_dtype, float cliprange,
-                                  float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb,
-                                  int64_t dst, float* dvalues, void* workspace, void* stream) {
-    RowArgs a = {};
-    const int rc = fill_loss_rows(&a, logits, dtype, B, T, V, sb, st, labels, lb, lt, old_lp, old_dtype, adv_raw,
-                                  stats, unbiased, mask, values, v_dtype, old_values, ov_dtype, returns, r_dtype,
-                                  cliprange, cliprange_value, vf_coef, lp_out, dx, dsb, dst, dvalues, workspace);
-    if (rc) return rc;
-    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
-}
-
-// A fused loss-rows launch with this step's GAE tail as its first workgroups: the GAE
-// writes adv_raw / returns / stats, the rows of the same launch wait for them (see
-// gae_block<true>).  old_lp is the experience log-prob (fp32) the GAE reads as lp.
-extern "C" int trlx_ppo_loss_rows_gae(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
-                                      int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
-                                      int old_dtype, float* adv_raw, double* stats, int unbiased,
-                                      const int64_t* mask, const void* values, int v_dtype, const void* old_values,
-                                      int ov_dtype, void* returns, int r_dtype, float cliprange,
-                                      float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb,
-                                      int64_t dst, float* dvalues, void* workspace, const float* ref_lp,
-                                      const float* scores, const int64_t* lengths, float kl_coef,
-                                      const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
-                                      void* stream) {
-    TRLX_REQUIRE(old_dtype == TRLX_F32 && r_dtype == TRLX_F32, TRLX_ERR_DTYPE,
-                 "trlx_ppo_loss_rows_gae: old_lp and returns must be fp32");
-    RowArgs a = {};
-    int rc = fill_loss_rows(&a, logits, dtype, B, T, V, sb, st, labels, lb, lt, old_lp, old_dtype, adv_raw, stats,
-                            unbiased, mask, values, v_dtype, old_values, ov_dtype, returns, r_dtype, cliprange,
-                            cliprange_value, vf_coef, lp_out, dx, dsb, dst, dvalues, workspace);
-    if (rc) return rc;
-    rc = fill_gae(&a.gae, B, T, static_cast<const float*>(old_lp), ref_lp, old_values, ov_dtype, scores, lengths,
-                  mask, kl_coef, ctl, gamma, lam, rewards, adv_raw, returns, r_dtype, stats, workspace);
-    if (rc) return rc;
-    a.has_gae = 1;
-    a.gae_ready = a.gae.ws.tickets + 2;
-    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
-}
-
-static int fill_loss_tail(LossRolloutArgs* L, int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
-                          float* loss_stats, void* workspace, const trlx_kl_ctl* kl);
-
-extern "C" int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int64_t B, int64_t T,
-                                             int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
-                                             int64_t lt, void* out_lp0, void* out_lp1, int out_dtype, int64_t tail_B,
-                                             int64_t tail_T, const double* tail_stats, float vf_coef, float* loss,
-                                             float* loss_stats, void* workspace, const trlx_kl_ctl* kl,
-                                             void* stream) {
-    RowArgs a = {};
-    a.x0 = x0; a.x1 = x1; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
-    a.labels = labels; a.lb = lb; a.lt = lt;
-    a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype;
-    int rc = fill_loss_tail(&a.tail, tail_B, tail_T, tail_stats, vf_coef, loss, loss_stats, workspace, kl);
-    if (rc) return rc;
-    a.has_tail = 1;
-    if (B * T == 0 && B >= 0 && T >= 0) return tail_standalone(a, (hipStream_t)stream);
-    rc = check_rows(a, dtype);
-    if (rc) return rc;
-    TRLX_REQUIRE(out_lp0 && (!x1 || out_lp1), TRLX_ERR_ARG, "NULL logprob output");
-    TRLX_REQUIRE(out_dtype == TRLX_F32 || out_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "out dtype");
-    return launch_rows<kFwd>(a, dtype, x1 ? 2 : 1, (hipStream_t)stream);
-}
-
-extern "C" int trlx_lsm_gather_bwd(const void* x, int dtype, int64_t B, int64_t T, int64_t V,
-                                   int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
-                                   int64_t lt, const float* lse, const void* grad, int grad_dtype,
-                                   void* dx, int64_t dsb, int64_t dst, void* stream) {
-    RowArgs a = {};
-    a.x0 = x; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
-    a.lse_in = lse; a.grad = grad; a.grad_dtype = grad_dtype; a.dx = dx; a.dsb = dsb; a.dst = dst;
-    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;
-    int rc = check_rows(a, dtype);
-    if (rc) return rc;
-    TRLX_REQUIRE(lse && grad && dx, TRLX_ERR_ARG, "NULL lse/grad/dx");
-    return launch_rows<kBwd>(a, dtype, 1, (hipStream_t)stream);
-}
-
-extern "C" int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_t T, int64_t V,
-                                     int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
-                                     int64_t lt, const void* old_lp, int old_dtype, const float* adv,
-                                     const double* stats, int unbiased, const int64_t* mask,
-                                     const double* msum, double msum_host, float cliprange,
-                                     float* lp_out, void* dx, int64_t dsb, int64_t dst, void* stream) {
-    RowArgs a = {};
-    a.x0 = x; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
-    a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv; a.stats = stats; a.unbiased = unbiased;
-    a.mask = mask; a.msum = msum; a.msum_host = msum_host; a.cliprange = cliprange;
-    a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
-    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;
-    int rc = check_rows(a, dtype);
-    if (rc) return rc;
-    TRLX_REQUIRE(old_lp && adv && lp_out && dx, TRLX_ERR_ARG, "NULL old_lp/adv/lp_out/dx");
-    TRLX_REQUIRE(msum || msum_host > 0, TRLX_ERR_ARG, "mask sum must be positive");
-    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
-}
-
-extern "C" int64_t trlx_ppo_workspace_bytes(int64_t B, int64_t T) {
-    return int64_t(carve_workspace(nullptr, B, T, nullptr));
-}
-
-static int fill_gae(GaeRolloutArgs* ep, int64_t B, int64_t T, const float* lp, const float* ref_lp,
-                    const void* values, int v_dtype, const float* scores, const int64_t* lengths,
-                    const int64_t* mask, float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam,
-                    float* rewards, float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace) {
-    TRLX_REQUIRE(B > 0 && T > 0 && B * T < (1LL << 31), TRLX_ERR_SHAPE, "bad rollout batch %lld x %lld",
-                 (long long)B, (long long)T);
-    TRLX_REQUIRE(lp && ref_lp && values && rewards && adv_raw && ret && stats && workspace, TRLX_ERR_ARG,
-                 "NULL argument to trlx_ppo_rollout_gae");
-    GaeRolloutArgs& e = *ep;
-    e = {};
-    carve_workspace(workspace, B, T, &e.ws);
-    e.B = int(B); e.T = int(T); e.lp = lp; e.ref_lp = ref_lp; e.values = values; e.v_dtype = v_dtype;
-    e.scores = scores; e.lengths = lengths; e.mask = mask; e.neg_beta = -kl_coef; e.gamma = gamma;
-    e.gl = float(double(gamma) * double(lam));  // python float product, then fp32 (torch scalar)
-    e.rewards = rewards; e.adv = adv_raw; e.ret = ret; e.ret_dtype = ret_dtype; e.stats = stats;
-    if (ctl) {
-        TRLX_REQUIRE(scores && ctl->state_in && ctl->state_out, TRLX_ERR_ARG,
-                     "score control needs scores, state_in and state_out");
-        TRLX_REQUIRE(ctl->state_in != ctl->state_out, TRLX_ERR_ARG,
-                     "trlx_ppo_rollout_gae_ctl: state_out must not alias state_in (every block reads it)");
-        TRLX_REQUIRE(ctl->scale_mode >= TRLX_SCALE_NONE && ctl->scale_mode <= TRLX_SCALE_REF, TRLX_ERR_ARG,
-                     "bad scale_mode %d", ctl->scale_mode);
-        e.has_ctl = 1;
-        e.ctl.state_in = ctl->state_in; e.ctl.state_out = ctl->state_out; e.ctl.global_mom = ctl->global_moments;
-        e.ctl.scale_mode = ctl->scale_mode; e.ctl.clip = ctl->cliprange_reward;
-    }
-    return TRLX_OK;
-}
-
-static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
-                            int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
-                            float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
-                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream) {
-    GaeRolloutArgs e;
-    const int rc = fill_gae(&e, B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, ctl, gamma, lam,
-                            rewards, adv_raw, ret, ret_dtype, stats, workspace);
-    if (rc) return rc;
-    const unsigned nblk = unsigned((B + kGaeRolloutsPerBlock - 1) / kGaeRolloutsPerBlock);
-    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kGaeThreads), 0, (hipStream_t)stream, e);
+    const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
+    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
     return check_launch("k_rollout_gae");
 }
 
@@ -1196,34 +911,6 @@ extern "C" int trlx_ppo_loss_rows(const void* logits, int dtype, int64_t B, int6
     a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
     a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
     a.ltok.dv = dvalues;
-    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
-}
-
-// A fused loss-rows launch with this step's GAE tail as its first workgroups: the GAE
-// writes adv_raw / returns / stats, the rows of the same launch wait for them (see
-// gae_block<true>).  old_lp is the experience log-prob (fp32) the GAE reads as lp.
-extern "C" int trlx_ppo_loss_rows_gae(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
-                                      int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
-                                      int old_dtype, float* adv_raw, double* stats, int unbiased,
-                                      const int64_t* mask, const void* values, int v_dtype, const void* old_values,
-                                      int ov_dtype, void* returns, int r_dtype, float cliprange,
-                                      float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb,
-                                      int64_t dst, float* dvalues, void* workspace, const float* ref_lp,
-                                      const float* scores, const int64_t* lengths, float kl_coef,
-                                      const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
-                                      void* stream) {
-    TRLX_REQUIRE(old_dtype == TRLX_F32 && r_dtype == TRLX_F32, TRLX_ERR_DTYPE,
-                 "trlx_ppo_loss_rows_gae: old_lp and returns must be fp32");
-    RowArgs a = {};
-    int rc = fill_loss_rows(&a, logits, dtype, B, T, V, sb, st, labels, lb, lt, old_lp, old_dtype, adv_raw, stats,
-                            unbiased, mask, values, v_dtype, old_values, ov_dtype, returns, r_dtype, cliprange,
-                            cliprange_value, vf_coef, lp_out, dx, dsb, dst, dvalues, workspace);
-    if (rc) return rc;
-    rc = fill_gae(&a.gae, B, T, static_cast<const float*>(old_lp), ref_lp, old_values, ov_dtype, scores, lengths,
-                  mask, kl_coef, ctl, gamma, lam, rewards, adv_raw, returns, r_dtype, stats, workspace);
-    if (rc) return rc;
-    a.has_gae = 1;
-    a.gae_ready = a.gae.ws.tickets + 2;
     return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
 }
 
