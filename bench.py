@@ -97,7 +97,74 @@ def parse():
                         "(comm.RcclComm: ncclAllReduce enqueued on the step's stream, no ProcessGroupNCCL event "
                         "joins); torch = torch.distributed.all_reduce; auto = rccl with the nccl backend, falling "
                         "back to torch (reported in config.comm) if the communicator cannot be created")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher rehearsal without a GPU: every rank joins a gloo group, checks its rank / world "
+                        "against the others and rank 0 prints one JSON line (tests/test_host_cpu.py)")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without an external launcher: start N child processes of this
+    script (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1) and
+    return the first non-zero exit code.  Runs BEFORE anything in this process touches the
+    GPU (torch is not even imported) and never execs: the parent only waits.  Rank 0's
+    stdout carries the JSON line; if a rank fails, the others are terminated by PID."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py launcher: rank {procs.index(p)} exited with {code}; stopping the others",
+                      file=sys.stderr)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def dry_run(args):
+    """Rehearse the rank layout of a multi-rank run on the CPU (gloo): each rank contributes
+    its RANK / LOCAL_RANK and rank 0 checks the group saw 0..N-1 exactly once."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        got = [None] * world
+        dist.all_gather_object(got, (rank, local))
+        dist.destroy_process_group()
+    else:
+        got = [(rank, local)]
+    if rank == 0:
+        ok = sorted(got) == [(r, r) for r in range(world)]
+        print(json.dumps({"dry_run": True, "n_gpus": world, "requested": args.gpus, "ranks": got, "ok": ok}),
+              flush=True)
+        if not ok:
+            raise SystemExit(3)
 
 
 def algorithmic_bytes(V, s, masked):
@@ -354,6 +421,12 @@ def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1, comm=Non
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: refusing a mislabelled run")
+    if args.dry_run:
+        return dry_run(args)
     import torch
     import torch.distributed as dist
     import __graft_entry__
@@ -366,8 +439,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     use_dist = world > 1 or args.dist

@@ -205,3 +205,24 @@ def test_hot_path_refuses_bad_loss_norm():
     import trlx_t5_amd as P
     with pytest.raises(ValueError):
         P.PPOHotPath(P.PPOConfig(), 2, 3, 5, torch.bfloat16, "cpu", kl_coef=0.05, loss_norm="batch")
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_launcher_spawns_ranks(n):
+    """`bench.py --gpus N` with no WORLD_SIZE starts N ranks itself (never a silent 1-rank
+    run); the dry run joins them in a gloo group and rank 0 prints one line with n_gpus N."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([__import__("sys").executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--dry-run"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    rec = __import__("json").loads(lines[0])
+    assert rec["n_gpus"] == n and rec["ok"] and sorted(map(tuple, rec["ranks"])) == [(i, i) for i in range(n)]
+
+
+def test_bench_refuses_mislabelled_world():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([__import__("sys").executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dry-run"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
