@@ -408,7 +408,7 @@ def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1, comm=Non
     cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
     ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
     pipelined = args.schedule == "pipelined" or (args.schedule == "auto" and world > 1)
-    defer = not (pipelined or args.overlap_tail or args.no_defer_tail)
+    defer = not (args.overlap_tail or args.no_defer_tail)  # pipelined too: split beta keeps its tail foldable
     hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=args.overlap_tail,
                       loss_norm=args.loss_norm, defer_tail=defer, comm=comm)
     fn = hp.pipeline_step if pipelined else hp.step  # pipelined: each call = E rows of one batch + loss of the last

@@ -49,6 +49,7 @@ typedef enum {
 
 /* Number of fp64 slots per partial-statistics record (see trlx_gae_scan). */
 #define TRLX_MOMENT_SLOTS 4     /* {sum x, sum x^2, count, sum mask} */
+#define TRLX_SPLIT_MOMENT_SLOTS 8 /* {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0} */
 /* Number of fp32 slots written by trlx_ppo_loss_finalize (order = stats keys of
  * PPOConfig.loss, ppo_models.py:182-198, after losses). */
 #define TRLX_PPO_STATS 13
@@ -433,6 +434,43 @@ int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int
                                   void* out_lp0, void* out_lp1, int out_dtype, int64_t tail_B, int64_t tail_T,
                                   const double* tail_stats, float vf_coef, float* loss, float* loss_stats,
                                   void* workspace, const trlx_kl_ctl* kl, void* stream);
+
+/* ---------------------------------------------------------------- split-beta step (DP pipeline)
+ * The KL-penalised reward r = score_t - beta*kl_t (ppo_orchestrator.py:163-167) enters GAE
+ * (ppo_models.py:121-139) linearly, so A = A0 - beta*Ak with A0 the GAE of the score +
+ * value terms and Ak the discounted KL sums.  Splitting them lets the GAE launch run before
+ * the previous batch's KL-controller update (accelerate_ppo_model.py:123,130-131), which the
+ * pipelined data-parallel schedule needs to keep its loss tail folded.
+ *   trlx_ppo_rollout_gae_split  one wave per rollout: adv0 = A0, adv_kl = Ak, rew_kl = kl_t
+ *       (0 past the length), rew_score = the score term (-0.0 before the last column, 0 past
+ *       it) and the split record stats8 = {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0}
+ *       (all-reduce the first 6, or 7 for a global loss normaliser).  ctl: score control as
+ *       in trlx_ppo_rollout_gae_ctl (may be NULL); beta is not read.  prev_stats8 (optional):
+ *       block 0 also writes the whitening coefficients of the PREVIOUS batch to prev_coef,
+ *       with beta = ctl->state_in[TRLX_CTL_KL_COEF] (or kl_coef without ctl).
+ *   trlx_ppo_whiten_coef  the same coefficients as a launch of its own (ctl_state may be NULL):
+ *       coef = {mean, rsqrt(var + 1e-8), beta, 0} of A = A0 - beta*Ak (modeling.py:24-34;
+ *       unbiased: torch.var_mean, else the distributed biased variance).
+ *   trlx_ppo_loss_rows_split  trlx_ppo_loss_rows with the advantage A0 - coef[2]*Ak whitened
+ *       by coef, the mask sum at *msum (stats8 + 6), and this batch's rewards
+ *       (-beta*rew_kl + rew_score) and returns (A + old_values, r_dtype) written here.  The
+ *       loss tail takes stats8 + 3 as its `stats` (it reads Σ mask at stats[3]). */
+int trlx_ppo_rollout_gae_split(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                               int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                               const trlx_score_ctl* ctl, float kl_coef, float gamma, float lam, float* adv0,
+                               float* adv_kl, float* rew_kl, float* rew_score, double* stats8,
+                               const double* prev_stats8, float* prev_coef, int prev_unbiased, void* workspace,
+                               void* stream);
+int trlx_ppo_whiten_coef(const double* stats8, int unbiased, const double* ctl_state, float kl_coef, float* coef,
+                         void* stream);
+int trlx_ppo_loss_rows_split(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
+                             int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
+                             int old_dtype, const float* adv0, const float* adv_kl, const float* rew_kl,
+                             const float* rew_score, const float* coef, const double* msum, const int64_t* mask,
+                             const void* values, int v_dtype, const void* old_values, int ov_dtype, float* rewards,
+                             void* returns, int r_dtype, float cliprange, float cliprange_value, float vf_coef,
+                             float* lp_out, void* dx, int64_t dsb, int64_t dst, float* dvalues, void* workspace,
+                             void* stream);
 
 /* ---------------------------------------------------------------- RCCL stats all-reduce helper
  * SURVEY §8b "Collectives" — replaces the two dist.all_reduce calls of

@@ -36,6 +36,13 @@ for st in $steps; do
             done ;;
         valu) run ${TAG}_pmc_valu_c2 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_TRANS_F32 SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/${TAG}_pmc_valu_c2 -o run -- $B --steps 5 --warmup 2 --settle-ms 0 --no-timers ;;
         tests) run ${TAG}_gpu_tests 900 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+        tsplit) run ${TAG}_gpu_tests_split 600 python3 -u -m pytest tests/test_gpu_split_beta.py tests/test_gpu_dist.py tests/test_gpu_rccl.py tests/test_gpu_control.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+        sched) for i in 1 2; do
+                 run ${TAG}_sched_serial_$i 200 $B --steps 200 --warmup 5
+                 run ${TAG}_sched_pipe_$i 200 $B --steps 200 --warmup 5 --schedule pipelined
+                 run ${TAG}_sched_rccl_serial_$i 200 $B --steps 200 --warmup 5 --dist --schedule serial
+                 run ${TAG}_sched_rccl_pipe_$i 200 $B --steps 200 --warmup 5 --dist --schedule pipelined
+               done ;;
         smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
         *) echo "unknown step $st"; exit 2 ;;
     esac

@@ -122,22 +122,27 @@ def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap):
                for k, v in b.items()} for b in batches]
     B, T, V = shards[0]["logits"].shape
     res = {}
-    for mode in ("serial", "pipelined"):
+    for mode in ("serial", "pipelined", "unsplit"):
         cfg = P.PPOConfig(scale_reward="running")
         ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B) if use_ctl else None
-        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, overlap_tail=overlap)
+        # "serial": step() with the split-beta kernels pipeline_step uses (bit-identical);
+        # "unsplit": the default step() kernels (equal up to fp32 association); defer the
+        # loss tails unless the side-stream tail is under test
+        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, overlap_tail=overlap,
+                          defer_tail=not overlap, split_beta=mode != "unsplit")
         outs = []
 
         def grab(o):
             loss, stats, dl, dv = o
             hp.wait_stats()
             torch.cuda.synchronize()
-            outs.append([loss.cpu().numpy(), stats.cpu().numpy(), dl.float().cpu().numpy(), dv.cpu().numpy()])
+            outs.append([loss.cpu().numpy(), stats.cpu().numpy(), dl.float().cpu().numpy(), dv.cpu().numpy(),
+                         hp.rewards.cpu().numpy(), hp.returns.cpu().numpy()])
 
         for sh in shards:
             args = (sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"], sh["old_values"], sh["values"],
                     sh["scores"])
-            if mode == "serial":
+            if mode != "pipelined":
                 grab(hp.step(*args, lengths=sh["lengths"], mask=sh["mask"]))
             else:
                 o = hp.pipeline_step(*args, lengths=sh["lengths"], mask=sh["mask"])
@@ -180,17 +185,18 @@ def rccl_world1_worker(port, inputs, xs_all, q):
         res["comm_rejects_f32"] = False
     except ValueError:
         res["comm_rejects_f32"] = True
-    for mode, kind in (("serial", "torch"), ("pipelined", "torch"), ("serial", "rccl"), ("pipelined", "rccl")):
+    for mode, kind in (("serial", "torch"), ("pipelined", "torch"), ("serial", "rccl"), ("pipelined", "rccl"),
+                       ("unsplit", "rccl")):
         cfg = P.PPOConfig()
         ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B)
         hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl,
-                          comm=comm if kind == "rccl" else None)
+                          comm=comm if kind == "rccl" else None, split_beta=mode != "unsplit")
         outs = []
         for b in inputs:
             xb = {k: (v.to(dev) if v is not None else None) for k, v in b.items()}
             args = (xb["logits"], xb["ref_logits"], xb["new_logits"], xb["labels"], xb["old_values"], xb["values"],
                     xb["scores"])
-            o = hp.step(*args) if mode == "serial" else hp.pipeline_step(*args)
+            o = hp.step(*args) if mode != "pipelined" else hp.pipeline_step(*args)
             if o is not None:
                 torch.cuda.synchronize()
                 outs.append([t.float().cpu().numpy() for t in o])

@@ -178,8 +178,9 @@ def test_dp2_step_global_loss_norm():
 @pytest.mark.parametrize("use_ctl,overlap,lengths", [(True, True, False), (False, False, True)])
 def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths):
     """PPOHotPath.pipeline_step (the DP schedule that hides the whitening all-reduce behind
-    the next batch's experience rows) against step() over three batches at world 2:
-    losses, stats, gradients and the device controller state bit-identical per batch."""
+    the next batch's experience rows; split-beta GAE) against step(split_beta=True) over three
+    batches at world 2: losses, stats, gradients, rewards, returns and the device controller
+    state bit-identical per batch; against the unsplit step() equal up to fp32 association."""
     import torch.multiprocessing as mp
     import dist_workers
     world, B, T, V = 2, 8, 21, 1031
@@ -197,9 +198,14 @@ def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths):
         assert p.exitcode == 0
     for r in range(world):
         (ser, ser_state), (pip, pip_state) = res[r]["serial"], res[r]["pipelined"]
-        assert len(ser) == len(pip) == len(batches)
+        uns, uns_state = res[r]["unsplit"]
+        assert len(ser) == len(pip) == len(uns) == len(batches)
         if use_ctl:
             assert np.array_equal(ser_state, pip_state), f"rank {r} controller state"
-        for i, (a, b) in enumerate(zip(ser, pip)):
-            for x, y in zip(a, b):
-                assert np.array_equal(x, y, equal_nan=True), f"rank {r} batch {i}"
+            np.testing.assert_allclose(uns_state, ser_state, rtol=1e-5)
+        for i, (a, b, c) in enumerate(zip(ser, pip, uns)):
+            for j, (x, y, z) in enumerate(zip(a, b, c)):
+                assert np.array_equal(x, y, equal_nan=True), f"rank {r} batch {i} output {j}"
+                # split beta vs the unsplit kernels: fp32 association only (dlogits: bf16)
+                np.testing.assert_allclose(z, x, rtol=2e-2 if j == 2 else 1e-4, atol=1e-5,
+                                           err_msg=f"rank {r} batch {i} output {j}")

@@ -2,9 +2,10 @@
 one GPU of the dev box — RCCL cannot put two ranks on one device, so N > 1 runs only on the
 driver's 8-GPU node; this pins everything short of the wire:
   * ProcessGroupNCCL initialised with device_id before any tensor is made (bench.py's order);
-  * PPOHotPath.step (blocking whitening all-reduce) and pipeline_step (async all-reduce, the
-    loss side waiting on RCCL's stream) give bit-identical losses, stats, gradients,
-    whitening record and controller state over three batches;
+  * PPOHotPath.step (blocking whitening all-reduce; split_beta=True, the kernels the pipeline
+    uses) and pipeline_step (async all-reduce, the loss side waiting on RCCL's stream) give
+    bit-identical losses, stats, gradients, whitening record and controller state over three
+    batches, and the unsplit step() the same numbers up to fp32 association;
   * the same two schedules through the boundary's RCCL helper (comm.RcclComm: ncclAllReduce
     enqueued on the step's stream / a side stream joined by fence-free events) are
     bit-identical to the torch.distributed ones;
@@ -57,6 +58,12 @@ def test_rccl_world1_hot_path_and_drop_in_surface(golden):
             for x, y in zip(a, b):
                 assert np.array_equal(x, y, equal_nan=True), key
         assert np.array_equal(ser_st, st) and np.array_equal(ser_ctl, ctl), key
+    # the unsplit kernels (step() default): the same numbers up to fp32 association
+    uns, _, uns_ctl = res[("unsplit", "rccl")]
+    for a, b in zip(ser, uns):
+        for i, (x, y) in enumerate(zip(a, b)):
+            np.testing.assert_allclose(y, x, rtol=2e-2 if i == 2 else 1e-4, atol=1e-5)
+    np.testing.assert_allclose(uns_ctl, ser_ctl, rtol=1e-5)
     for k, (mean, var, count, w, w2) in res["surface"].items():
         bf = k == "bf16"
         assert count == float(z[f"{k}/dist1/count"])

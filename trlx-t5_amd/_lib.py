@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libtrlx_t5_amd.so")
 F32, BF16, I64 = 0, 1, 2
 ABI_VERSION = 1
 MOMENT_SLOTS = 4
+SPLIT_MOMENT_SLOTS = 8  # split-beta record {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0}
 PPO_STATS = 13
 PPO_PARTIAL_SLOTS = 16
 
@@ -126,6 +127,14 @@ SIGNATURES = {
                                           _score_ctl_p, _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                           _c_vp]),
     "trlx_ppo_rollout_loss_ctl": (_c_int, [_c_i64, _c_i64, _c_vp, _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
+    "trlx_ppo_rollout_gae_split": (_c_int, [_c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
+                                            _score_ctl_p, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                            _c_vp, _c_vp, _c_int, _c_vp, _c_vp]),
+    "trlx_ppo_whiten_coef": (_c_int, [_c_vp, _c_int, _c_vp, _c_f, _c_vp, _c_vp]),
+    "trlx_ppo_loss_rows_split": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
+                                          _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                          _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_f, _c_f, _c_f,
+                                          _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
     "trlx_comm_load": (_c_int, [ctypes.c_char_p]),
     "trlx_comm_unique_id_bytes": (_c_i64, []),
     "trlx_comm_unique_id": (_c_int, [_c_vp, _c_i64]),

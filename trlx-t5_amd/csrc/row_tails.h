@@ -30,7 +30,7 @@ __device__ __forceinline__ double wave_allsum_d(double v) {
 
 // Workspace carve-up (16-B aligned sections), see trlx_ppo_workspace_bytes:
 //   tickets : uint32[4]                    (zero before first use; re-armed in-kernel)
-//   gae_rec : double[nblk][4]              per-block moments
+//   gae_rec : double[nblk][8]              per-block moments (4 used unless split-beta)
 //   loss_rec: double[nblk][16]             per-block loss sums
 //   tokrec  : float[B*T][kTokRec]          per-token loss terms
 struct Workspace {
@@ -55,23 +55,58 @@ struct GaeRolloutArgs {
     float* adv;               // [B,T] fp32 out (unwhitened)
     void* ret;                // [B,T] out
     int ret_dtype;
-    double* stats;            // [4] out
+    double* stats;            // [4] out ([8] split-beta)
     Workspace ws;
     int has_ctl;              // score/beta control from the device state (ctl_state.h)
     ScoreCtlArgs ctl;
+    // split-beta GAE (k_rollout_gae<true>): beta-free outputs, beta applied by the loss rows
+    float* adv_kl;            // [B,T] out: GAE suffix sums of the KL term (the "A_k" part)
+    float* rew_kl;            // [B,T] out: lp - ref_lp (0 past the rollout's length)
+    float* rew_score;         // [B,T] out: score term (the score at the last column, -0.0 before it, 0 past it)
+    // optional: whitening coefficients of the PREVIOUS batch, folded into this launch
+    const double* prev_stats; // [8] split record of that batch (all-reduced) or NULL
+    float* prev_coef;         // [4] out {mu, rstd, beta, 0}
+    int prev_unbiased;
+    float host_beta;          // beta without device controller state
 };
+
+// Split-beta whitening coefficients: the KL-penalised reward is r = score_t - beta*kl_t and
+// GAE is linear in r, so A = A0 - beta*Ak with A0 the GAE of the score + value terms and Ak
+// the discounted KL sums.  The split record {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0}
+// gives Σ A = Σ A0 - beta Σ Ak and Σ A² = Σ A0² - 2 beta Σ A0·Ak + beta² Σ Ak² in fp64, then
+// the same {sum, sumsq, n} whitening as the unsplit path (modeling.py:24-34).
+__device__ __forceinline__ void whiten_coef_split(const double* st, int unbiased, float beta, float* coef) {
+    const double b = double(beta);
+    const double rec[3] = {fma(-b, st[3], st[0]), fma(b * b, st[5], fma(-2.0 * b, st[4], st[1])), st[2]};
+    float mu, rstd;
+    whiten_coeffs(rec, unbiased, mu, rstd);
+    coef[0] = mu;
+    coef[1] = rstd;
+    coef[2] = beta;
+    coef[3] = 0.0f;
+}
 
 // KL reward (ppo_orchestrator.py:164-167, score on the last valid column) and GAE
 // (ppo_models.py:128-136) for one rollout: the suffix recurrence A_t = δ_t + c·A_{t+1} as a
 // lane-parallel scan (log2 64 steps) per 64-token chunk from the end, the carry
 // A_{chunk end} entering with weight c^(n).  fp32 re-association vs the reference's
 // sequential loop: ~1e-7 relative.
+//
+// SPLIT (split-beta, the pipelined DP schedule): beta is not needed here.  The scan runs
+// twice on the same lanes — A0 over δ0 = score_t + γ·V_{t+1} − V_t and Ak over kl_t — and
+// the block record carries the split moments (whiten_coef_split); rewards, returns and
+// whitening are finished by the loss rows once beta is known, so this launch no longer
+// waits for the previous batch's KL-controller update.  Block 0 may also emit the
+// previous batch's whitening coefficients (prev_stats -> prev_coef) with the beta the
+// state holds now.
+template <bool SPLIT>
 __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs e) {
-    __shared__ double red[kRolloutsPerBlock * TRLX_MOMENT_SLOTS];
+    constexpr int NS = SPLIT ? 8 : TRLX_MOMENT_SLOTS;
+    __shared__ double red[kRolloutsPerBlock * NS];
     const int lane = threadIdx.x & (kWave - 1);
     const int b = blockIdx.x * kRolloutsPerBlock + threadIdx.x / kWave;
     const int T = e.T;
-    double s1 = 0.0, s2 = 0.0, sm = 0.0, cnt = 0.0;
+    double s1 = 0.0, s2 = 0.0, sm = 0.0, cnt = 0.0, sk = 0.0, sak = 0.0, skk = 0.0;
     float neg_beta = e.neg_beta, sdiv = 0.0f, sclip = 0.0f;
     // Device controller state: with a score scale every block needs the merged statistics
     // up front (each derives the same values; block 0 stores them).  Without one (the
@@ -86,38 +121,65 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
         neg_beta = -float(e.ctl.state_in[TRLX_CTL_KL_COEF]);
     }
     if (e.has_ctl) sclip = e.ctl.clip;
+    if (SPLIT && e.prev_stats && blockIdx.x == 0 && threadIdx.x == 0)
+        whiten_coef_split(e.prev_stats, e.prev_unbiased, e.has_ctl ? float(e.ctl.state_in[TRLX_CTL_KL_COEF]) : e.host_beta,
+                          e.prev_coef);
     if (b < e.B) {
         const int len = e.lengths ? int(e.lengths[b]) : T;
         const float log2c = e.gl > 0.0f ? __log2f(e.gl) : -INFINITY;
-        float carry = 0.0f, vcarry = 0.0f;  // A and V just past the current chunk
+        float carry = 0.0f, vcarry = 0.0f, kcarry = 0.0f;  // A (A0, Ak) and V just past the current chunk
         for (int c0 = ((T - 1) / kWave) * kWave; c0 >= 0; c0 -= kWave) {
             const int t = c0 + lane;
             const bool ok = t < T;
             const int64_t gi = int64_t(b) * T + t;
-            float v = 0.0f, r = 0.0f;
+            float v = 0.0f, r = 0.0f, kl = 0.0f, sc = 0.0f;
             if (ok && t < len) {
                 v = ld_any(e.values, e.v_dtype, gi);
-                r = mul_rn(neg_beta, e.lp[gi] - e.ref_lp[gi]);
-                if (t == len - 1 && e.scores) r = add_rn(r, score_transform(e.scores[b], sdiv, sclip));
+                kl = e.lp[gi] - e.ref_lp[gi];
+                sc = -0.0f;  // x + (-0.0) == x: the loss rows' add leaves a score-free reward as is
+                if (t == len - 1 && e.scores) sc = score_transform(e.scores[b], sdiv, sclip);
+                if (!SPLIT) {
+                    r = mul_rn(neg_beta, kl);
+                    if (t == len - 1 && e.scores) r = add_rn(r, sc);
+                }
             }
             float vn = __shfl_down(v, 1, kWave);
             if (lane == kWave - 1) vn = vcarry;
-            const float delta = ok ? add_rn(r, mul_rn(e.gamma, vn)) - v : 0.0f;
-            float x = delta, cd = e.gl;
+            const float delta = ok ? add_rn(SPLIT ? sc : r, mul_rn(e.gamma, vn)) - v : 0.0f;
+            float x = delta, xk = kl, cd = e.gl;
 #pragma unroll
             for (int d = 1; d < kWave; d <<= 1) {
                 const float y = __shfl_down(x, d, kWave);
                 if (lane + d < kWave) x = fmaf(cd, y, x);
+                if (SPLIT) {
+                    const float yk = __shfl_down(xk, d, kWave);
+                    if (lane + d < kWave) xk = fmaf(cd, yk, xk);
+                }
                 cd = cd * cd;
             }
             const int end = min(c0 + kWave, T);
-            const float A = ok ? fmaf(exp2_fast(float(end - t) * log2c), carry, x) : 0.0f;
+            const float cw = exp2_fast(float(end - t) * log2c);
+            const float A = ok ? fmaf(cw, carry, x) : 0.0f;
             carry = __shfl(A, 0, kWave);
             vcarry = __shfl(v, 0, kWave);
+            float Ak = 0.0f;
+            if (SPLIT) {
+                Ak = ok ? fmaf(cw, kcarry, xk) : 0.0f;
+                kcarry = __shfl(Ak, 0, kWave);
+            }
             if (ok) {
-                e.rewards[gi] = r;
                 e.adv[gi] = A;
-                st_any(e.ret, e.ret_dtype, gi, add_rn(A, v));
+                if (SPLIT) {
+                    e.adv_kl[gi] = Ak;
+                    e.rew_kl[gi] = kl;
+                    e.rew_score[gi] = t < len ? sc : 0.0f;
+                    sk += double(Ak);
+                    sak += double(A) * double(Ak);
+                    skk += double(Ak) * double(Ak);
+                } else {
+                    e.rewards[gi] = r;
+                    st_any(e.ret, e.ret_dtype, gi, add_rn(A, v));
+                }
                 s1 += double(A);
                 s2 += double(A) * double(A);
                 sm += e.mask ? double(e.mask[gi]) : 1.0;
@@ -129,14 +191,27 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
         float d_unused, b_unused;
         score_ctl_block(e.ctl, e.scores, e.B, true, d_unused, b_unused);
     }
-    const double mine[TRLX_MOMENT_SLOTS] = {s1, s2, cnt, sm};
-    const double rec = block_sum_multi<TRLX_MOMENT_SLOTS>(mine, red);
-    if (publish_record_last<TRLX_MOMENT_SLOTS>(e.ws.gae_rec + blockIdx.x * TRLX_MOMENT_SLOTS, rec,
-                                               e.ws.tickets + 0, gridDim.x)) {
-        __syncthreads();  // red[] reuse
-        const double tot = reduce_records<TRLX_MOMENT_SLOTS>(e.ws.gae_rec, gridDim.x, red);
-        if (threadIdx.x < TRLX_MOMENT_SLOTS) e.stats[threadIdx.x] = tot;
+    double mine[NS];
+    if constexpr (SPLIT) {  // {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0}
+        mine[0] = s1; mine[1] = s2; mine[2] = cnt; mine[3] = sk; mine[4] = sak; mine[5] = skk; mine[6] = sm;
+        mine[7] = 0.0;
+    } else {
+        mine[0] = s1; mine[1] = s2; mine[2] = cnt; mine[3] = sm;
     }
+    const double rec = block_sum_multi<NS>(mine, red);
+    if (publish_record_last<NS>(e.ws.gae_rec + blockIdx.x * NS, rec, e.ws.tickets + 0, gridDim.x)) {
+        __syncthreads();  // red[] reuse
+        const double tot = reduce_records<NS>(e.ws.gae_rec, gridDim.x, red);
+        if (threadIdx.x < NS) e.stats[threadIdx.x] = tot;
+    }
+}
+
+// The split-beta whitening coefficients as a launch of its own (one thread): the serial
+// split schedule, and the last batch of a pipelined sequence (nothing left to fold it into).
+__global__ void k_whiten_coef(const double* stats, int unbiased, const double* ctl_state, float host_beta,
+                              float* coef) {
+    if (threadIdx.x == 0)
+        whiten_coef_split(stats, unbiased, ctl_state ? float(ctl_state[TRLX_CTL_KL_COEF]) : host_beta, coef);
 }
 
 // ------------------------------------------------------------------ loss sums per rollout

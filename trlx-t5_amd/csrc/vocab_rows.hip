@@ -57,6 +57,13 @@ struct RowArgs {
     // `tail_blocks` workgroups (trlx_lsm_gather_fwd_loss_tail); row = blockIdx.x - tail_blocks
     int has_tail, tail_blocks;
     LossRolloutArgs tail;
+    // split-beta loss rows (trlx_ppo_loss_rows_split): adv = A0, A = A0 - beta*Ak whitened with
+    // coef {mu, rstd, beta}; this launch also finishes the batch's rewards and returns
+    const float* coef;
+    const float* adv_kl;
+    const float* rew_kl;
+    const float* rew_score;
+    float* rewards_out;
 };
 
 // ------------------------------------------------------------------ shared row pieces
@@ -89,13 +96,38 @@ struct Row {
 struct PpoScalars {
     float A, m, inv_msum, olp;
 };
-__device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row) {
+// Split beta: the token's value-loss inputs {values, old_values, returns}, with the return
+// A + V (ppo_models.py:135) finished here from A = A0 - beta*Ak and stored (thread 0).
+__device__ __forceinline__ void split_value_inputs(const RowArgs& a, int64_t row, float A, float* vin) {
+    vin[0] = ld_any(a.ltok.values, a.ltok.v_dtype, row);
+    vin[1] = ld_any(a.ltok.old_values, a.ltok.ov_dtype, row);
+    const float R = add_rn(A, vin[1]);
+    if (threadIdx.x == 0) st_any(const_cast<void*>(a.ltok.returns), a.ltok.r_dtype, row, R);
+    vin[2] = a.ltok.r_dtype == TRLX_BF16 ? bf2f(f2bf(R)) : R;  // the value loss sees the stored return
+}
+__device__ __forceinline__ float split_advantage(const RowArgs& a, int64_t row) {
+    return a.adv[row] - mul_rn(a.coef[2], a.adv_kl[row]);
+}
+
+// vin (fused loss, tokrec set): {values, old_values, returns} of the token's value loss,
+// loaded here when `early` (the resident rows park them in LDS; the streaming rows load
+// them after the row).
+__device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row, float* vin, bool early) {
     PpoScalars p;
     p.A = a.adv[row];
-    if (a.stats) {
+    if (a.coef) {  // split beta: this token's advantage, reward and return are finished here
+        const float mu = a.coef[0], rstd = a.coef[1], beta = a.coef[2];
+        const float A = split_advantage(a, row);
+        if (threadIdx.x == 0) a.rewards_out[row] = add_rn(mul_rn(-beta, a.rew_kl[row]), a.rew_score[row]);
+        p.A = mul_rn(A - mu, rstd);
+        if (early && a.tokrec) split_value_inputs(a, row, A, vin);
+    } else if (a.stats) {
         float mu, rstd;
         whiten_coeffs(a.stats, a.unbiased, mu, rstd);
         p.A = mul_rn(p.A - mu, rstd);
+        if (early && a.tokrec) loss_token_inputs(a.ltok, row, vin);
+    } else if (early && a.tokrec) {
+        loss_token_inputs(a.ltok, row, vin);
     }
     p.m = a.mask ? float(a.mask[row]) : 1.0f;
     const double msum = a.msum ? *a.msum : a.msum_host;
@@ -162,9 +194,10 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     // occupy no VGPRs beside the row.
     __shared__ float s_ps[7];
     if (MODE == kPpo && tid == 0) {
-        const PpoScalars p0 = ppo_scalars(a, r.row);
+        float vin[3];
+        const PpoScalars p0 = ppo_scalars(a, r.row, vin, true);
         s_ps[0] = p0.A; s_ps[1] = p0.m; s_ps[2] = p0.inv_msum; s_ps[3] = p0.olp;
-        if (a.tokrec) loss_token_inputs(a.ltok, r.row, s_ps + 4);
+        if (a.tokrec) { s_ps[4] = vin[0]; s_ps[5] = vin[1]; s_ps[6] = vin[2]; }
     }
 
     const int nvec = int(r.s.nvec);
@@ -427,7 +460,8 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
     const int tid = threadIdx.x, nthr = blockDim.x;
     const Row<DT> r(a);
     PpoScalars ps = {0.f, 1.f, 1.f, 0.f};
-    if (MODE == kPpo) ps = ppo_scalars(a, r.row);
+    float vin[3];
+    if (MODE == kPpo) ps = ppo_scalars(a, r.row, vin, false);
     const vec4u* vp = reinterpret_cast<const vec4u*>(r.x + r.s.head);
     const int64_t nvec = r.s.nvec;
     const int64_t je = r.edge_index();
@@ -536,8 +570,10 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
     }
     if (je >= 0) DT::store1(drow, je, je == r.y ? gy : ng * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
     if (MODE == kPpo && a.tokrec && tid == 0) {
-        float vin[3];
-        loss_token_inputs(a.ltok, r.row, vin);
+        if (a.coef)
+            split_value_inputs(a, r.row, split_advantage(a, r.row), vin);
+        else
+            loss_token_inputs(a.ltok, r.row, vin);
         token_record(a, r.row, pt, ps, vin);
     }
 }
@@ -736,7 +772,7 @@ static size_t carve_workspace(void* base, int64_t B, int64_t T, Workspace* w) {
     if (w) w->tickets = reinterpret_cast<unsigned*>(p + off);
     off += 16;
     if (w) w->gae_rec = reinterpret_cast<double*>(p + off);
-    off += ws_align(sizeof(double) * TRLX_MOMENT_SLOTS * size_t(nblk));
+    off += ws_align(sizeof(double) * 8 * size_t(nblk));  // split-beta records are 8 wide
     if (w) w->loss_rec = reinterpret_cast<double*>(p + off);
     off += ws_align(sizeof(double) * 16 * size_t(nblk));
     if (w) w->tokrec = reinterpret_cast<float*>(p + off);
@@ -825,13 +861,22 @@ extern "C" int64_t trlx_ppo_workspace_bytes(int64_t B, int64_t T) {
     return int64_t(carve_workspace(nullptr, B, T, nullptr));
 }
 
+// Split-beta outputs of the GAE launch (k_rollout_gae<true>); NULL = the unsplit launch.
+struct SplitGae {
+    float *adv_kl, *rew_kl, *rew_score;
+    const double* prev_stats;
+    float* prev_coef;
+    int prev_unbiased;
+};
+
 static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
                             int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
                             float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
-                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream) {
+                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream,
+                            const SplitGae* sp = nullptr) {
     TRLX_REQUIRE(B > 0 && T > 0 && B * T < (1LL << 31), TRLX_ERR_SHAPE, "bad rollout batch %lld x %lld",
                  (long long)B, (long long)T);
-    TRLX_REQUIRE(lp && ref_lp && values && rewards && adv_raw && ret && stats && workspace, TRLX_ERR_ARG,
+    TRLX_REQUIRE(lp && ref_lp && values && adv_raw && stats && workspace && (sp || (rewards && ret)), TRLX_ERR_ARG,
                  "NULL argument to trlx_ppo_rollout_gae");
     GaeRolloutArgs e = {};
     carve_workspace(workspace, B, T, &e.ws);
@@ -850,8 +895,18 @@ static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* 
         e.ctl.state_in = ctl->state_in; e.ctl.state_out = ctl->state_out; e.ctl.global_mom = ctl->global_moments;
         e.ctl.scale_mode = ctl->scale_mode; e.ctl.clip = ctl->cliprange_reward;
     }
+    if (sp) {
+        TRLX_REQUIRE(sp->adv_kl && sp->rew_kl && sp->rew_score, TRLX_ERR_ARG, "NULL split-beta GAE output");
+        TRLX_REQUIRE(!sp->prev_stats || sp->prev_coef, TRLX_ERR_ARG, "prev_stats needs prev_coef");
+        e.adv_kl = sp->adv_kl; e.rew_kl = sp->rew_kl; e.rew_score = sp->rew_score;
+        e.prev_stats = sp->prev_stats; e.prev_coef = sp->prev_coef; e.prev_unbiased = sp->prev_unbiased;
+        e.host_beta = kl_coef;
+    }
     const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
-    hipLaunchKernelGGL(k_rollout_gae, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
+    if (e.adv_kl)
+        hipLaunchKernelGGL(k_rollout_gae<true>, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
+    else
+        hipLaunchKernelGGL(k_rollout_gae<false>, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
     return check_launch("k_rollout_gae");
 }
 
@@ -871,6 +926,25 @@ extern "C" int trlx_ppo_rollout_gae_ctl(int64_t B, int64_t T, const float* lp, c
     TRLX_REQUIRE(ctl, TRLX_ERR_ARG, "NULL trlx_score_ctl");
     return rollout_gae_impl(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, 0.0f, ctl, gamma, lam,
                             rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
+}
+
+extern "C" int trlx_ppo_rollout_gae_split(int64_t B, int64_t T, const float* lp, const float* ref_lp,
+                                          const void* values, int v_dtype, const float* scores,
+                                          const int64_t* lengths, const int64_t* mask, const trlx_score_ctl* ctl,
+                                          float kl_coef, float gamma, float lam, float* adv0, float* adv_kl,
+                                          float* rew_kl, float* rew_score, double* stats8, const double* prev_stats8,
+                                          float* prev_coef, int prev_unbiased, void* workspace, void* stream) {
+    const SplitGae sp = {adv_kl, rew_kl, rew_score, prev_stats8, prev_coef, prev_unbiased};
+    return rollout_gae_impl(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, ctl, gamma, lam,
+                            nullptr, adv0, nullptr, TRLX_F32, stats8, workspace, stream, &sp);
+}
+
+extern "C" int trlx_ppo_whiten_coef(const double* stats8, int unbiased, const double* ctl_state, float kl_coef,
+                                    float* coef, void* stream) {
+    TRLX_REQUIRE(stats8 && coef, TRLX_ERR_ARG, "NULL argument to trlx_ppo_whiten_coef");
+    hipLaunchKernelGGL(k_whiten_coef, dim3(1), dim3(kWave), 0, (hipStream_t)stream, stats8, unbiased, ctl_state,
+                       kl_coef, coef);
+    return check_launch("k_whiten_coef");
 }
 
 extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dtype, int64_t B,
@@ -905,6 +979,36 @@ extern "C" int trlx_ppo_loss_rows(const void* logits, int dtype, int64_t B, int6
     TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
     TRLX_REQUIRE(old_lp && adv_raw && stats && values && old_values && returns && lp_out && dx && dvalues && workspace,
                  TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_rows");
+    Workspace ws;
+    carve_workspace(workspace, B, T, &ws);
+    a.tokrec = ws.tokrec;
+    a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
+    a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
+    a.ltok.dv = dvalues;
+    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
+}
+
+extern "C" int trlx_ppo_loss_rows_split(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
+                                        int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
+                                        int old_dtype, const float* adv0, const float* adv_kl, const float* rew_kl,
+                                        const float* rew_score, const float* coef, const double* msum,
+                                        const int64_t* mask, const void* values, int v_dtype, const void* old_values,
+                                        int ov_dtype, float* rewards, void* returns, int r_dtype, float cliprange,
+                                        float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb,
+                                        int64_t dst, float* dvalues, void* workspace, void* stream) {
+    RowArgs a = {};
+    a.x0 = logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
+    a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv0; a.adv_kl = adv_kl; a.rew_kl = rew_kl;
+    a.rew_score = rew_score; a.coef = coef; a.rewards_out = rewards;
+    a.mask = mask; a.msum = msum; a.msum_host = double(B * T); a.cliprange = cliprange;
+    a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
+    int rc = check_rows(a, dtype);
+    if (rc) return rc;
+    TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
+    TRLX_REQUIRE(old_lp && adv0 && adv_kl && rew_kl && rew_score && coef && rewards && values && old_values &&
+                 returns && lp_out && dx && dvalues && workspace, TRLX_ERR_ARG,
+                 "NULL argument to trlx_ppo_loss_rows_split");
+    TRLX_REQUIRE(r_dtype == TRLX_F32 || r_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "returns dtype %d", r_dtype);
     Workspace ws;
     carve_workspace(workspace, B, T, &ws);
     a.tokrec = ws.tokrec;

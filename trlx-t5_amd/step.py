@@ -66,8 +66,15 @@ class PPOHotPath:
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
                  device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
                  ctl: Optional[PPOControlState] = None, overlap_tail: bool = False, loss_norm: str = "rank",
-                 defer_tail: bool = False, comm: Optional[RcclComm] = None):
+                 defer_tail: bool = False, comm: Optional[RcclComm] = None, split_beta: bool = False):
         self.cfg = cfg
+        # split_beta: step() runs the split-beta GAE / loss rows (trlx_ppo_rollout_gae_split,
+        # trlx_ppo_loss_rows_split) that pipeline_step always uses: A = A0 - beta*Ak, beta
+        # applied by the loss rows.  Same arithmetic as pipeline_step, so the two schedules
+        # agree bit for bit; the unsplit kernels differ from it only by fp32 association.
+        self.split_beta = bool(split_beta)
+        self._sbuf = None  # split-beta buffer sets (two: the pipeline's batches k and k+1)
+        self._sidx = 0     # the set the current batch uses
         # comm: the boundary's RCCL helper (comm.RcclComm) for the step's all-reduces instead
         # of torch.distributed — enqueued on the step's stream (blocking schedule) or on a side
         # stream joined with fence-free events (pipelined schedule, score moments)
@@ -112,11 +119,15 @@ class PPOHotPath:
         self.lp_old = torch.empty((B, T), **f32)
         self.ref_lp = torch.empty((B, T), **f32)
         self.rewards = torch.empty((B, T), **f32)
-        self.adv_raw = torch.empty((B, T), **f32)
+        self.adv_raw = self._adv_raw4 = torch.empty((B, T), **f32)  # split-beta: the set's A0
         self.returns = torch.empty((B, T), dtype=value_dtype, device=self.device)
         self.lp_new = torch.empty((B, T), **f32)
         self.dvalues = torch.empty((B, T), **f32)
-        self.adv_stats = torch.empty(_lib.MOMENT_SLOTS, dtype=torch.float64, device=self.device)
+        self._stats4 = torch.empty(_lib.MOMENT_SLOTS, dtype=torch.float64, device=self.device)
+        self.adv_stats = self._stats4  # the current batch's whitening record (split-beta: its 8-slot set)
+        self._split_mode = False  # how the current batch's GAE ran (the loss launch must match)
+        self._coef_ready = False  # split: the batch's whitening coefficients were folded into a GAE launch
+        self._ar_msum = None      # global loss norm: the Σmask slot of the record in flight
         self.loss = torch.empty(1, **f32)
         self.stats = torch.empty(_lib.PPO_STATS, **f32)
         nbytes = _lib.query("trlx_ppo_workspace_bytes", B, T)
@@ -257,10 +268,27 @@ class PPOHotPath:
         B, T, V = self.B, self.T, self.V
         labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
         s = torch.cuda.current_stream(self.device)
+        self._use_split(self.split_beta, 0)
         g_mom, work = self._begin_step(scores, group, s)
         self._experience_rows(logits, ref_logits, labels, s)
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
         return self.lp_old, self.ref_lp
+
+    def _use_split(self, split, idx):
+        """Select the unsplit GAE / loss kernels or the split-beta ones with buffer set `idx`."""
+        self._split_mode, self._sidx, self._coef_ready = bool(split), idx, False
+        if split and self._sbuf is None:
+            f32 = dict(dtype=torch.float32, device=self.device)
+            self._sbuf = [dict(adv0=torch.empty((self.B, self.T), **f32), adv_kl=torch.empty((self.B, self.T), **f32),
+                               rew_kl=torch.empty((self.B, self.T), **f32),
+                               rew_score=torch.empty((self.B, self.T), **f32),
+                               stats=torch.zeros(_lib.SPLIT_MOMENT_SLOTS, dtype=torch.float64, device=self.device),
+                               coef=torch.zeros(4, **f32)) for _ in range(2)]
+        if split:
+            sb = self._sbuf[idx]
+            self.adv_stats, self.adv_raw = sb["stats"], sb["adv0"]
+        else:
+            self.adv_stats, self.adv_raw = self._stats4, self._adv_raw4
 
     def _experience_rows(self, logits, ref_logits, labels, s):
         B, T, V = self.B, self.T, self.V
@@ -270,7 +298,7 @@ class PPOHotPath:
         self._ev("experience", s)
         if self._tail_pending is not None:  # the previous step's loss tail rides this launch
             pend, self._tail_pending = self._tail_pending, None
-            _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, *pend, s.cuda_stream)
+            _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, *self._tail_args(pend), s.cuda_stream)
         else:
             _lib.call("trlx_lsm_gather_fwd", *rows, None, None, s.cuda_stream)
         self._ev_end("experience", s)
@@ -279,11 +307,18 @@ class PPOHotPath:
         """Run a deferred loss tail by itself (nothing to fold it into)."""
         if self._tail_pending is None:
             return
-        (B, T, st, vf, loss, stats, ws, kl), self._tail_pending = self._tail_pending, None
+        pend, self._tail_pending = self._tail_pending, None
+        B, T, st, vf, loss, stats, ws, kl = self._tail_args(pend)
         if kl is not None:
             _lib.call("trlx_ppo_rollout_loss_ctl", B, T, st, vf, loss, stats, ws, kl, s.cuda_stream)
         else:
             _lib.call("trlx_ppo_rollout_loss", B, T, st, vf, loss, stats, ws, s.cuda_stream)
+
+    def _tail_args(self, pend):
+        """A deferred loss tail's arguments, its KL-controller record resolved NOW: the tail
+        updates beta in the record current when it runs (after any GAE launch that advanced
+        the double-buffered state in between — the split-beta pipeline's order)."""
+        return pend + ((self.ctl.kl_ctl() if self.ctl is not None else None),)
 
     # hidden size from which the fused lm_head loses to hipBLASLt + the rows kernel
     # (profiles/r01_lmhead_route_sweep.log: fused 1.00-1.08x at H <= 1024, 0.93-0.95x from
@@ -331,6 +366,7 @@ class PPOHotPath:
                                    lengths=lengths, mask=mask, group=group)
         s = torch.cuda.current_stream(self.device)
         self._launch_pending_tail(s)
+        self._use_split(self.split_beta, 0)
         g_mom, work = self._begin_step(scores, group, s)
         N = B * T
         nbytes = _lib.query("trlx_lmhead_workspace_bytes", N, V)
@@ -350,35 +386,49 @@ class PPOHotPath:
         return self.lp_old, self.ref_lp
 
     def _experience_tail(self, s, labels, old_values, scores, lengths, mask, group, g_mom, work,
-                         defer_allreduce=False):
+                         defer_allreduce=False, fold=None):
+        """GAE tail (+ the whitening all-reduce).  Split-beta mode: trlx_ppo_rollout_gae_split
+        into the current buffer set; `fold` = the previous set, whose whitening coefficients
+        this launch also emits (the pipelined schedule)."""
         B, T = self.B, self.T
         if work is not None:
             work.wait()
-        if self.tail_done is not None:  # previous loss tail: reads adv_stats[3] + token records, updates beta
+        if self.tail_done is not None:  # previous loss tail: reads Σmask + token records, updates beta
             self.tail_done.wait(s)
         self._ev("rollout_gae", s)
         tail = (B, T, self.lp_old.data_ptr(), self.ref_lp.data_ptr(), old_values.data_ptr(),
                 _lib.dtype_code(old_values), _lib.ptr(scores), _lib.ptr(lengths), _lib.ptr(mask))
-        outs = (float(self.cfg.gamma), float(self.cfg.lam), self.rewards.data_ptr(), self.adv_raw.data_ptr(),
-                self.returns.data_ptr(), _lib.dtype_code(self.returns), self.adv_stats.data_ptr(),
-                self.workspace.data_ptr(), s.cuda_stream)
-        if self.ctl is not None:
-            _lib.call("trlx_ppo_rollout_gae_ctl", *tail, self.ctl.score_ctl(g_mom), *outs)
+        if self._split_mode:
+            sb = self._sbuf[self._sidx]
+            prev = (fold["stats"].data_ptr(), fold["coef"].data_ptr(), 0 if self.distributed else 1) \
+                if fold is not None else (None, None, 0)
+            _lib.call("trlx_ppo_rollout_gae_split", *tail, self.ctl.score_ctl(g_mom) if self.ctl is not None else None,
+                      self.kl_coef, float(self.cfg.gamma), float(self.cfg.lam), sb["adv0"].data_ptr(),
+                      sb["adv_kl"].data_ptr(), sb["rew_kl"].data_ptr(), sb["rew_score"].data_ptr(),
+                      sb["stats"].data_ptr(), *prev, self.workspace.data_ptr(), s.cuda_stream)
+            # {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak²} (+ Σmask for the global loss normaliser)
+            rec, msum = sb["stats"][:7 if self.loss_norm == "global" else 6], sb["stats"][6:7]
         else:
-            _lib.call("trlx_ppo_rollout_gae", *tail, self.kl_coef, *outs)
+            outs = (float(self.cfg.gamma), float(self.cfg.lam), self.rewards.data_ptr(), self.adv_raw.data_ptr(),
+                    self.returns.data_ptr(), _lib.dtype_code(self.returns), self.adv_stats.data_ptr(),
+                    self.workspace.data_ptr(), s.cuda_stream)
+            if self.ctl is not None:
+                _lib.call("trlx_ppo_rollout_gae_ctl", *tail, self.ctl.score_ctl(g_mom), *outs)
+            else:
+                _lib.call("trlx_ppo_rollout_gae", *tail, self.kl_coef, *outs)
+            # {Σ A, Σ A², n} (+ Σmask for the global loss normaliser): the only data-path exchange
+            rec, msum = self.adv_stats[:4 if self.loss_norm == "global" else 3], self.adv_stats[3:4]
         self._ev_end("rollout_gae", s)
         if self.distributed:
-            # {Σ A, Σ A², n} (+ Σmask for the global loss normaliser): the only data-path exchange
-            k = 4 if self.loss_norm == "global" else 3
-            self._ar_group = group
+            self._ar_group, self._ar_msum = group, msum
             if self.comm is not None:
                 if defer_allreduce:  # issued with the next batch's score moments (_begin_step)
-                    self._ar_unissued, self._ar_work = self.adv_stats[:k], None
+                    self._ar_unissued, self._ar_work = rec, None
                 else:  # on the step's own stream: ordered with no join at all
-                    self.comm.allreduce_(self.adv_stats[:k], s)
+                    self.comm.allreduce_(rec, s)
                     self._ar_work = _StreamJoin(None, self.device)
             else:
-                self._ar_work = dist.all_reduce(self.adv_stats[:k], dist.ReduceOp.SUM, group=group, async_op=True)
+                self._ar_work = dist.all_reduce(rec, dist.ReduceOp.SUM, group=group, async_op=True)
             if not defer_allreduce:
                 self._resolve_allreduce()
 
@@ -394,7 +444,7 @@ class PPOHotPath:
         w.wait()
         if self.loss_norm == "global":
             world = self.comm.nranks if self.comm is not None else dist.get_world_size(self._ar_group)
-            self.adv_stats[3:4].div_(world)
+            self._ar_msum.div_(world)
 
     # -------------------------------------------------------------- K2
     def policy_loss(self, new_logits, labels, values, old_values, mask=None):
@@ -415,15 +465,33 @@ class PPOHotPath:
         if self.tail_done is not None:
             self.tail_done.wait(s)
         dx = self.dlogits
-        self._ev("loss", s)
-        _lib.call("trlx_ppo_loss_rows", new_logits.data_ptr(), _lib.dtype_code(new_logits), B, T, V,
-                  new_logits.stride(0), new_logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1),
-                  self.lp_old.data_ptr(), _lib.F32, self.adv_raw.data_ptr(), self.adv_stats.data_ptr(),
-                  0 if self.distributed else 1, _lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values),
-                  old_values.data_ptr(), _lib.dtype_code(old_values), self.returns.data_ptr(),
-                  _lib.dtype_code(self.returns), float(self.cfg.cliprange), float(self.cfg.cliprange_value),
-                  float(self.cfg.vf_coef), self.lp_new.data_ptr(), dx.data_ptr(), dx.stride(0), dx.stride(1),
-                  self.dvalues.data_ptr(), self.workspace.data_ptr(), s.cuda_stream)
+        rows = (new_logits.data_ptr(), _lib.dtype_code(new_logits), B, T, V, new_logits.stride(0),
+                new_logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1), self.lp_old.data_ptr(),
+                _lib.F32)
+        grads = (float(self.cfg.cliprange), float(self.cfg.cliprange_value), float(self.cfg.vf_coef),
+                 self.lp_new.data_ptr(), dx.data_ptr(), dx.stride(0), dx.stride(1), self.dvalues.data_ptr(),
+                 self.workspace.data_ptr(), s.cuda_stream)
+        if self._split_mode:
+            sb = self._sbuf[self._sidx]
+            if not self._coef_ready:  # not folded into a GAE launch: the coefficients as their own launch
+                _lib.call("trlx_ppo_whiten_coef", sb["stats"].data_ptr(), 0 if self.distributed else 1,
+                          self.ctl.state.data_ptr() if self.ctl is not None else None, self.kl_coef,
+                          sb["coef"].data_ptr(), s.cuda_stream)
+            self._coef_ready = True  # a second loss on this experience (ppo_epochs) reuses them
+            self._ev("loss", s)
+            _lib.call("trlx_ppo_loss_rows_split", *rows, sb["adv0"].data_ptr(), sb["adv_kl"].data_ptr(),
+                      sb["rew_kl"].data_ptr(), sb["rew_score"].data_ptr(), sb["coef"].data_ptr(),
+                      sb["stats"].data_ptr() + 6 * 8, _lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values),
+                      old_values.data_ptr(), _lib.dtype_code(old_values), self.rewards.data_ptr(),
+                      self.returns.data_ptr(), _lib.dtype_code(self.returns), *grads)
+            tail_stats = sb["stats"].data_ptr() + 3 * 8  # the tail reads Σmask at stats[3]
+        else:
+            self._ev("loss", s)
+            _lib.call("trlx_ppo_loss_rows", *rows, self.adv_raw.data_ptr(), self.adv_stats.data_ptr(),
+                      0 if self.distributed else 1, _lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values),
+                      old_values.data_ptr(), _lib.dtype_code(old_values), self.returns.data_ptr(),
+                      _lib.dtype_code(self.returns), *grads)
+            tail_stats = self.adv_stats.data_ptr()
         self._ev_end("loss", s)
         ts = s
         if self.tail_stream is not None:
@@ -431,10 +499,10 @@ class PPOHotPath:
             rows_done.record(s)
             ts = self.tail_stream
             rows_done.wait(ts)
-        args = (B, T, self.adv_stats.data_ptr(), float(self.cfg.vf_coef), self.loss.data_ptr(),
-                self.stats.data_ptr(), self.workspace.data_ptr())
+        args = (B, T, tail_stats, float(self.cfg.vf_coef), self.loss.data_ptr(), self.stats.data_ptr(),
+                self.workspace.data_ptr())
         if self.defer_tail:  # runs inside the next experience launch (or wait_stats)
-            self._tail_pending = args + ((self.ctl.kl_ctl() if self.ctl is not None else None),)
+            self._tail_pending = args
             return self.loss, self.stats, self.dlogits, self.dvalues
         self._ev("rollout_loss", ts)
         if self.ctl is not None:  # + kl_ctl.update(approx_kl) (accelerate_ppo_model.py:123,130-131)
@@ -468,18 +536,23 @@ class PPOHotPath:
     # -------------------------------------------------------------- pipelined schedule (DP > 1)
     def pipeline_step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
                       lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None):
-        """Software-pipelined step for data parallelism: the experience rows of THIS batch run
-        while the previous batch's whitening all-reduce is in flight, then the previous
-        batch's loss, then this batch's GAE tail and its all-reduce (async):
+        """Software-pipelined step for data parallelism.  Per call (batch k+1):
 
-            E rows(k+1) | [AR(k) in flight] -> L rows(k) + loss tail(k) -> GAE tail(k+1) -> AR(k+1) ...
+            E rows(k+1) [+ loss tail(k-1)] | [AR(k) in flight beside them]
+              -> join AR(k) -> GAE(k+1) [+ whitening coefficients of batch k] -> AR(k+1) async
+              -> L rows(k)  [loss tail(k) deferred into the next E launch]
 
-        Every data dependency of step() is kept (GAE(k+1) still follows loss tail(k), whose
-        KL-controller update it reads), so losses, stats, gradients and controller state are
-        bit-identical to calling step() per batch (tests/test_gpu_dist.py); only the RCCL
-        latency leaves the critical path.  Returns the PREVIOUS batch's (loss, stats,
-        dlogits, dvalues) — valid until the next call — or None on the first call;
-        pipeline_flush() runs the last pending loss.  lp_old / ref_lp are double-buffered."""
+        Split beta (trlx_ppo_rollout_gae_split): the reward r = score - beta*kl enters GAE
+        linearly, so GAE(k+1) runs before the KL-controller update of loss tail(k) and the
+        loss rows apply beta (A = A0 - beta*Ak, rewards, returns).  Every loss sees the beta
+        the serial schedule would give it, so losses, stats, gradients and controller state
+        are bit-identical to step() with split_beta=True (tests/test_gpu_dist.py) and equal to
+        the unsplit step() up to fp32 association.  The whitening all-reduce of batch k runs
+        while the experience rows of batch k+1 stream; nothing else waits on the network.
+        Returns the PREVIOUS batch's (loss, stats, dlogits, dvalues) — valid until the next
+        call; with defer_tail, loss / stats are final after wait_stats() — or None on the
+        first call; pipeline_flush() runs the last pending loss.  lp_old / ref_lp and the
+        split buffers are double-buffered."""
         self._check(logits)
         self._check(ref_logits)
         if logits.stride() != ref_logits.stride():
@@ -493,34 +566,39 @@ class PPOHotPath:
         labels, lengths, mask = (t if t is None or t is o else t.clone() for t, o in zip((labels, lengths, mask), orig))
         if self._lp_bufs is None:
             self._lp_bufs = [(self.lp_old, self.ref_lp), (torch.empty_like(self.lp_old), torch.empty_like(self.ref_lp))]
-            self._pb = 0
         prev = self._pending
-        nb = self._pb ^ 1 if prev is not None else self._pb
+        nb = prev["buf"] ^ 1 if prev is not None else 0
         s = torch.cuda.current_stream(self.device)
-        g_mom, work = self._begin_step(scores, group, s)
+        self._use_split(True, nb)
+        g_mom, work = self._begin_step(scores, group, s)  # + AR(k) on the side stream (RCCL helper)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
-        self._experience_rows(logits, ref_logits, labels, s)
-        out = self._pending_loss(s)
+        self._experience_rows(logits, ref_logits, labels, s)  # + the deferred loss tail(k-1)
+        self._resolve_allreduce()  # AR(k): GAE(k+1) folds batch k's whitening coefficients
+        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work, defer_allreduce=True,
+                              fold=self._sbuf[prev["buf"]] if prev is not None else None)
+        out = None
+        if prev is not None:
+            self._sidx, self._coef_ready = prev["buf"], True
+            self.adv_stats, self.adv_raw = self._sbuf[prev["buf"]]["stats"], self._sbuf[prev["buf"]]["adv0"]
+            self.lp_old, self.ref_lp = self._lp_bufs[prev["buf"]]
+            out = self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
+                                   mask=prev["mask"])
+        self._use_split(True, nb)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
-        self._launch_pending_tail(s)  # this batch's GAE tail reads the beta it updates
-        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work, defer_allreduce=True)
         self._pending = dict(buf=nb, new_logits=new_logits, labels=labels, values=values, old_values=old_values,
                              mask=mask)
-        self._pb = nb
         return out
-
-    def _pending_loss(self, s):
-        prev, self._pending = self._pending, None
-        if prev is None:
-            return None
-        self.lp_old, self.ref_lp = self._lp_bufs[prev["buf"]]
-        self._resolve_allreduce()
-        return self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
-                                mask=prev["mask"])
 
     def pipeline_flush(self):
         """Run the pending loss of the last pipeline_step batch; returns its outputs (or None)."""
-        return self._pending_loss(torch.cuda.current_stream(self.device))
+        prev, self._pending = self._pending, None
+        if prev is None:
+            return None
+        self._use_split(True, prev["buf"])
+        self.lp_old, self.ref_lp = self._lp_bufs[prev["buf"]]
+        self._resolve_allreduce()  # nothing left to hide it behind
+        return self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
+                                mask=prev["mask"])
 
     def step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
              lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None,
