@@ -139,10 +139,12 @@ def test_experience_from_hidden_vs_oracle():
     assert torch.isfinite(loss).all() and torch.isfinite(dl.float()).all()
 
 
-@pytest.mark.parametrize("H,route", [(192, "gemm"), (2048, "auto"), (192, "auto")])
-def test_experience_from_hidden_routes(H, route):
+@pytest.mark.parametrize("H,route,chunk", [(192, "gemm", None), (2048, "auto", None), (192, "auto", None),
+                                           (192, "gemm", 14), (2048, "auto", 20)])
+def test_experience_from_hidden_routes(H, route, chunk):
     """The GEMM route of experience_from_hidden (hipBLASLt bf16 logits + the experience rows
-    kernel; "auto" picks it from H >= LM_HEAD_GEMM_MIN_H) against the oracle on the
+    kernel over rollout chunks of LM_HEAD_CHUNK_TOKENS tokens — `chunk` forces 2-rollout
+    chunks with a ragged last one; "auto" picks it from H >= LM_HEAD_GEMM_MIN_H) against the oracle on the
     bf16-rounded logits the reference's bf16 lm_head produces (ppo_models.py:640 then
     modeling.py:37-41), and against the fused route on the same inputs.  Tolerance: the GEMM
     accumulates in fp32 before rounding to bf16, so a logit may land one bf16 ulp away from
@@ -160,10 +162,14 @@ def test_experience_from_hidden_routes(H, route):
     scores = torch.randn(B, generator=g) * 5
     args = [t.to(DEV) for t in (h, w, hr, wr, labels, old_values, scores)]
     hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    if chunk:
+        hp.LM_HEAD_CHUNK_TOKENS = chunk
     hp.experience_from_hidden(*args, route=route)
     torch.cuda.synchronize()
     expect_gemm = route == "gemm" or H >= P.PPOHotPath.LM_HEAD_GEMM_MIN_H
     assert (hp.lm_logits is not None) == expect_gemm
+    if expect_gemm:  # the ring holds one chunk of rollouts, never the whole batch
+        assert hp.lm_logits.shape == (2, min(B, max(1, (chunk or hp.LM_HEAD_CHUNK_TOKENS) // T)), T, V)
     lp, ref_lp, rew = hp.lp_old.cpu().double(), hp.ref_lp.cpu().double(), hp.rewards.cpu()
     logits = (h.double() @ w.double().t()).to(torch.bfloat16).double()
     ref_logits = (hr.double() @ wr.double().t()).to(torch.bfloat16).double()

@@ -290,18 +290,21 @@ class PPOHotPath:
         else:
             self.adv_stats, self.adv_raw = self._stats4, self._adv_raw4
 
-    def _experience_rows(self, logits, ref_logits, labels, s):
-        B, T, V = self.B, self.T, self.V
+    def _experience_rows(self, logits, ref_logits, labels, s, b0=0, timed=True):
+        """Policy + reference rows of rollouts [b0, b0 + logits.shape[0]) -> lp_old, ref_lp."""
+        B, T, V = logits.shape[0], self.T, self.V
         rows = (logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V, logits.stride(0),
-                logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1), self.lp_old.data_ptr(),
-                self.ref_lp.data_ptr(), _lib.F32)
-        self._ev("experience", s)
+                logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1), self.lp_old[b0].data_ptr(),
+                self.ref_lp[b0].data_ptr(), _lib.F32)
+        if timed:
+            self._ev("experience", s)
         if self._tail_pending is not None:  # the previous step's loss tail rides this launch
             pend, self._tail_pending = self._tail_pending, None
             _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, *self._tail_args(pend), s.cuda_stream)
         else:
             _lib.call("trlx_lsm_gather_fwd", *rows, None, None, s.cuda_stream)
-        self._ev_end("experience", s)
+        if timed:
+            self._ev_end("experience", s)
 
     def _launch_pending_tail(self, s):
         """Run a deferred loss tail by itself (nothing to fold it into)."""
@@ -324,6 +327,11 @@ class PPOHotPath:
     # (profiles/r01_lmhead_route_sweep.log: fused 1.00-1.08x at H <= 1024, 0.93-0.95x from
     # H = 1536 up to UL2's 4096)
     LM_HEAD_GEMM_MIN_H = 1280
+    # gemm route: logits of at most this many tokens per model exist at a time (a ring of
+    # [2, chunk, T, V] bf16, 0.5 GB at V = 32128 instead of [2, B, T, V]); measured at the C4
+    # shard (profiles/r03_lmhead_chunk.log): 4096-token chunks 1.006x the full-batch GEMM + rows,
+    # 2048 0.979x, 1024 0.904x (hipBLASLt loses efficiency on short M)
+    LM_HEAD_CHUNK_TOKENS = 4096
 
     def experience_from_hidden(self, hidden, weight, ref_hidden, ref_weight, labels, old_values, scores,
                                lengths=None, mask=None, group=None, route="auto"):
@@ -341,7 +349,8 @@ class PPOHotPath:
         the reference's bf16 lm_head does (ppo_models.py:615,640); "fused" keeps the fp32 MFMA
         accumulator (closer to exact).  lp therefore moves by up to ~1 bf16 ulp of the logits
         between the routes (tests/test_gpu_lmhead.py pins both against fp64 at realistic logit
-        scale).  The gemm route keeps a [2, B, T, V] bf16 buffer; release_lm_logits() frees it."""
+        scale).  The gemm route keeps a [2, chunk, T, V] bf16 ring (LM_HEAD_CHUNK_TOKENS tokens per
+        chunk: the full [2, B, T, V] logits never exist); release_lm_logits() frees it."""
         B, T, V = self.B, self.T, self.V
         for h, w in ((hidden, weight), (ref_hidden, ref_weight)):
             if h.dim() != 3 or tuple(h.shape[:2]) != (B, T) or w.dim() != 2 or w.shape[0] != V or \
@@ -356,15 +365,26 @@ class PPOHotPath:
         if route == "auto":
             long_k = min(hidden.shape[2], ref_hidden.shape[2]) >= self.LM_HEAD_GEMM_MIN_H
             route = "gemm" if long_k and self.dtype == torch.bfloat16 else "fused"
-        if route == "gemm":
-            _lib.require_cuda(hidden, weight, ref_hidden, ref_weight)
-            if self.lm_logits is None:
-                self.lm_logits = torch.empty((2, B, T, V), dtype=torch.bfloat16, device=self.device)
-            torch.matmul(hidden, weight.t(), out=self.lm_logits[0])
-            torch.matmul(ref_hidden, ref_weight.t(), out=self.lm_logits[1])
-            return self.experience(self.lm_logits[0], self.lm_logits[1], labels, old_values, scores,
-                                   lengths=lengths, mask=mask, group=group)
         s = torch.cuda.current_stream(self.device)
+        if route == "gemm":
+            # rollout chunks: hipBLASLt writes the chunk's policy and reference logits into the
+            # ring, one rows launch reads both (the deferred loss tail rides the first)
+            _lib.require_cuda(hidden, weight, ref_hidden, ref_weight)
+            cb = max(1, min(B, self.LM_HEAD_CHUNK_TOKENS // T))
+            if self.lm_logits is None or self.lm_logits.shape[1] != cb:
+                self.lm_logits = torch.empty((2, cb, T, V), dtype=torch.bfloat16, device=self.device)
+            self._use_split(self.split_beta, 0)
+            g_mom, work = self._begin_step(scores, group, s)
+            self._ev("experience", s)
+            for b0 in range(0, B, cb):
+                nb = min(cb, B - b0)
+                x0, x1 = self.lm_logits[0, :nb], self.lm_logits[1, :nb]
+                torch.matmul(hidden[b0:b0 + nb], weight.t(), out=x0)
+                torch.matmul(ref_hidden[b0:b0 + nb], ref_weight.t(), out=x1)
+                self._experience_rows(x0, x1, labels[b0:b0 + nb], s, b0=b0, timed=False)
+            self._ev_end("experience", s)
+            self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
+            return self.lp_old, self.ref_lp
         self._launch_pending_tail(s)
         self._use_split(self.split_beta, 0)
         g_mom, work = self._begin_step(scores, group, s)
@@ -516,7 +536,7 @@ class PPOHotPath:
         return self.loss, self.stats, self.dlogits, self.dvalues
 
     def release_lm_logits(self):
-        """Free the gemm route's resident [2, B, T, V] logits buffer (re-allocated on next use)."""
+        """Free the gemm route's [2, chunk, T, V] logits ring (re-allocated on next use)."""
         self.lm_logits = None
 
     def wait_stats(self, stream=None):
