@@ -12,7 +12,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtrlx_t5_amd.so")
+# TRLX_T5_AMD_LIB: another build of the same library (A/B tooling only, e.g. scripts/ab_rows.sh)
+LIB_PATH = os.environ.get("TRLX_T5_AMD_LIB") or os.path.join(_HERE, "libtrlx_t5_amd.so")
 
 F32, BF16, I64 = 0, 1, 2
 ABI_VERSION = 1
