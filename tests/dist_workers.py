@@ -29,7 +29,7 @@ def whiten_stats_worker(rank, world, port, xs, q):
     dist.destroy_process_group()
 
 
-def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank"):
+def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank", mode="step"):
     """One rank of a DP PPO step on cuda:0 over gloo (the product's exchange: the whitening
     record all-reduce inside PPOHotPath.experience).  Rank r takes the contiguous row block
     r of the batch (accelerate_ppo_model.py:146-148 sharding)."""
@@ -41,13 +41,18 @@ def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank"):
     sh = {k: (v.chunk(world, dim=0)[rank].contiguous().to(dev) if v is not None else None) for k, v in inputs.items()}
     B, T, V = sh["logits"].shape
     hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05, loss_norm=loss_norm)
-    loss, stats, dlogits, dvalues = hp.step(sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"],
-                                            sh["old_values"], sh["values"], sh["scores"], lengths=sh["lengths"],
-                                            mask=sh["mask"])
+    args = (sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"], sh["old_values"], sh["values"],
+            sh["scores"])
+    if mode == "pipelined":  # split-beta schedule: one batch through pipeline_step + flush
+        assert hp.pipeline_step(*args, lengths=sh["lengths"], mask=sh["mask"]) is None
+        loss, stats, dlogits, dvalues = hp.pipeline_flush()
+    else:
+        loss, stats, dlogits, dvalues = hp.step(*args, lengths=sh["lengths"], mask=sh["mask"])
+    hp.wait_stats()
     torch.cuda.synchronize()
     q.put((rank, {"lp": hp.lp_old.cpu(), "rewards": hp.rewards.cpu(), "adv_stats": hp.adv_stats.cpu(),
                   "loss": loss.cpu(), "dlogits": dlogits.float().cpu(), "dvalues": dvalues.cpu(),
-                  "stats": stats.cpu()}))
+                  "stats": stats.cpu(), "returns": hp.returns.cpu()}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -108,7 +113,7 @@ def drop_in_surface_worker(rank, world, port, xs_all, q):
     dist.destroy_process_group()
 
 
-def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap):
+def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap, loss_norm="rank"):
     """The same sequence of batches through PPOHotPath.step (serial) and
     PPOHotPath.pipeline_step (experience of batch k+1 ahead of the loss of batch k, the
     whitening all-reduce in flight meanwhile) on this rank's row shards.  Returns every
@@ -129,7 +134,7 @@ def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap):
         # "unsplit": the default step() kernels (equal up to fp32 association); defer the
         # loss tails unless the side-stream tail is under test
         hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, overlap_tail=overlap,
-                          defer_tail=not overlap, split_beta=mode != "unsplit")
+                          defer_tail=not overlap, split_beta=mode != "unsplit", loss_norm=loss_norm)
         outs = []
 
         def grab(o):

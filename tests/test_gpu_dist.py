@@ -33,16 +33,20 @@ def _inputs(B, T, V, seed, lengths):
                 values=values, scores=scores, lengths=L, mask=mask)
 
 
-@pytest.mark.parametrize("lengths", [False, True])
-def test_dp2_step_global_whitening(lengths):
+@pytest.mark.parametrize("lengths,mode", [(False, "step"), (True, "step"), (False, "pipelined"), (True, "pipelined")])
+def test_dp2_step_global_whitening(lengths, mode):
+    """Two ranks vs the oracle on the concatenated batch: the whitening moments all-reduced
+    (modeling.py:9-21), per-rank losses / gradients on each shard.  mode "pipelined": the
+    split-beta schedule (pipeline_step), its split record {Σ A0, Σ A0², n, Σ Ak, ...}."""
     import torch.multiprocessing as mp
     import dist_workers
     world, B, T, V = 2, 8, 20, 1031
     x = _inputs(B, T, V, 5 + lengths, lengths)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 300
-    ps = [ctx.Process(target=dist_workers.hot_path_step_worker, args=(r, world, port, x, q)) for r in range(world)]
+    port = 29500 + (os.getpid() + (37 if mode == "pipelined" else 0)) % 300
+    ps = [ctx.Process(target=dist_workers.hot_path_step_worker, args=(r, world, port, x, q, "rank", mode))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=180) for _ in range(world))
@@ -66,7 +70,9 @@ def test_dp2_step_global_whitening(lengths):
         torch.testing.assert_close(got["rewards"], rewards[rows], rtol=1e-5, atol=1e-5)
         st = got["adv_stats"]
         assert float(st[2]) == B * T  # the all-reduced count covers both shards
-        torch.testing.assert_close(st[0], adv.double().sum(), rtol=1e-5, atol=1e-5)
+        sum_a = st[0] - float(np.float32(0.05)) * st[3] if mode == "pipelined" else st[0]  # split: Σ A0 - beta Σ Ak
+        torch.testing.assert_close(sum_a, adv.double().sum(), rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(got["returns"], ret[rows], rtol=1e-5, atol=2e-5)
         xg = f["new_logits"][rows].clone().requires_grad_(True)
         vg = x["values"][rows].clone().requires_grad_(True)
         new_lp = orc.logprobs_from_logits(xg, x["labels"][rows])
@@ -175,12 +181,14 @@ def test_dp2_step_global_loss_norm():
     torch.testing.assert_close(mean_loss, loss.detach(), rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("use_ctl,overlap,lengths", [(True, True, False), (False, False, True)])
-def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths):
+@pytest.mark.parametrize("use_ctl,overlap,lengths,loss_norm", [(True, True, False, "rank"), (False, False, True, "rank"),
+                                                               (True, False, True, "global")])
+def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths, loss_norm):
     """PPOHotPath.pipeline_step (the DP schedule that hides the whitening all-reduce behind
     the next batch's experience rows; split-beta GAE) against step(split_beta=True) over three
     batches at world 2: losses, stats, gradients, rewards, returns and the device controller
-    state bit-identical per batch; against the unsplit step() equal up to fp32 association."""
+    state bit-identical per batch; against the unsplit step() equal up to fp32 association.
+    With loss_norm="global" the Σmask of the split record rides the all-reduce (slot 6)."""
     import torch.multiprocessing as mp
     import dist_workers
     world, B, T, V = 2, 8, 21, 1031
@@ -188,8 +196,8 @@ def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + (os.getpid() + 151) % 300
-    ps = [ctx.Process(target=dist_workers.pipeline_worker, args=(r, world, port, batches, q, use_ctl, overlap))
-          for r in range(world)]
+    ps = [ctx.Process(target=dist_workers.pipeline_worker, args=(r, world, port, batches, q, use_ctl, overlap,
+                                                                 loss_norm)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(world))
