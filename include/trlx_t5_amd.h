@@ -447,7 +447,10 @@ int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int
  *       (all-reduce the first 6, or 7 for a global loss normaliser).  ctl: score control as
  *       in trlx_ppo_rollout_gae_ctl (may be NULL); beta is not read.  prev_stats8 (optional):
  *       block 0 also writes the whitening coefficients of the PREVIOUS batch to prev_coef,
- *       with beta = ctl->state_in[TRLX_CTL_KL_COEF] (or kl_coef without ctl).
+ *       with beta = ctl->state_in[TRLX_CTL_KL_COEF] (or kl_coef without ctl).  mom_lag = 1:
+ *       ctl->global_moments are the PREVIOUS batch's all-reduced score moments, merged into
+ *       RunningMoments now (NULL: none yet); not with TRLX_SCALE_RUNNING.  done_event (a
+ *       hipEvent_t or NULL) is recorded by the launch's own dispatch.
  *   trlx_ppo_whiten_coef  the same coefficients as a launch of its own (ctl_state may be NULL):
  *       coef = {mean, rsqrt(var + 1e-8), beta, 0} of A = A0 - beta*Ak (modeling.py:24-34;
  *       unbiased: torch.var_mean, else the distributed biased variance).
@@ -459,8 +462,14 @@ int trlx_ppo_rollout_gae_split(int64_t B, int64_t T, const float* lp, const floa
                                int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
                                const trlx_score_ctl* ctl, float kl_coef, float gamma, float lam, float* adv0,
                                float* adv_kl, float* rew_kl, float* rew_score, double* stats8,
-                               const double* prev_stats8, float* prev_coef, int prev_unbiased, void* workspace,
-                               void* stream);
+                               const double* prev_stats8, float* prev_coef, int prev_unbiased, int mom_lag,
+                               void* workspace, void* stream, void* done_event);
+/* RunningMoments merge of an all-reduced {Σx, Σx², n} score record into the controller
+ * state (state_out may alias state_in): the last merge of a pipelined sequence whose GAE
+ * launches merged each batch's moments one batch late (mom_lag = 1 above: the scores are not
+ * scaled by the running std, so the merge can wait for the moments' all-reduce to hide
+ * behind the next batch's rows). */
+int trlx_score_moments_merge(const double* state_in, double* state_out, const double* moments, void* stream);
 int trlx_ppo_whiten_coef(const double* stats8, int unbiased, const double* ctl_state, float kl_coef, float* coef,
                          void* stream);
 int trlx_ppo_loss_rows_split(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,

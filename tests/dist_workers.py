@@ -113,7 +113,7 @@ def drop_in_surface_worker(rank, world, port, xs_all, q):
     dist.destroy_process_group()
 
 
-def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap, loss_norm="rank"):
+def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap, loss_norm="rank", scale="running"):
     """The same sequence of batches through PPOHotPath.step (serial) and
     PPOHotPath.pipeline_step (experience of batch k+1 ahead of the loss of batch k, the
     whitening all-reduce in flight meanwhile) on this rank's row shards.  Returns every
@@ -128,8 +128,10 @@ def pipeline_worker(rank, world, port, batches, q, use_ctl, overlap, loss_norm="
     B, T, V = shards[0]["logits"].shape
     res = {}
     for mode in ("serial", "pipelined", "unsplit"):
-        cfg = P.PPOConfig(scale_reward="running")
+        cfg = P.PPOConfig(scale_reward=scale)
         ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B) if use_ctl else None
+        # scale False / "ref": pipeline_step merges each batch's score moments one batch late
+        # (lag), the final controller state is still the serial one
         # "serial": step() with the split-beta kernels pipeline_step uses (bit-identical);
         # "unsplit": the default step() kernels (equal up to fp32 association); defer the
         # loss tails unless the side-stream tail is under test

@@ -181,14 +181,17 @@ def test_dp2_step_global_loss_norm():
     torch.testing.assert_close(mean_loss, loss.detach(), rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("use_ctl,overlap,lengths,loss_norm", [(True, True, False, "rank"), (False, False, True, "rank"),
-                                                               (True, False, True, "global")])
-def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths, loss_norm):
+@pytest.mark.parametrize("use_ctl,overlap,lengths,loss_norm,scale", [
+    (True, True, False, "rank", "running"), (False, False, True, "rank", "running"),
+    (True, False, True, "global", "running"), (True, False, False, "rank", False), (True, False, True, "rank", "ref")])
+def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths, loss_norm, scale):
     """PPOHotPath.pipeline_step (the DP schedule that hides the whitening all-reduce behind
     the next batch's experience rows; split-beta GAE) against step(split_beta=True) over three
     batches at world 2: losses, stats, gradients, rewards, returns and the device controller
     state bit-identical per batch; against the unsplit step() equal up to fp32 association.
-    With loss_norm="global" the Σmask of the split record rides the all-reduce (slot 6)."""
+    With loss_norm="global" the Σmask of the split record rides the all-reduce (slot 6).
+    scale False / "ref": RunningMoments merges each batch's score moments one batch late
+    inside the pipeline (lag), the final controller state equals the serial one."""
     import torch.multiprocessing as mp
     import dist_workers
     world, B, T, V = 2, 8, 21, 1031
@@ -197,7 +200,7 @@ def test_dp2_pipelined_schedule_matches_serial(use_ctl, overlap, lengths, loss_n
     q = ctx.Queue()
     port = 29500 + (os.getpid() + 151) % 300
     ps = [ctx.Process(target=dist_workers.pipeline_worker, args=(r, world, port, batches, q, use_ctl, overlap,
-                                                                 loss_norm)) for r in range(world)]
+                                                                 loss_norm, scale)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(world))

@@ -172,7 +172,8 @@ def test_whiten_coef_matches_fold():
     P._lib.call("trlx_ppo_rollout_gae_split", B, Tn, lp.data_ptr(), rlp.data_ptr(), ov.data_ptr(), P._lib.F32,
                 cuda(x["scores"]).data_ptr(), None, None, None, 0.05, 1.0, 0.95, sb1["adv0"].data_ptr(),
                 sb1["adv_kl"].data_ptr(), sb1["rew_kl"].data_ptr(), sb1["rew_score"].data_ptr(),
-                sb1["stats"].data_ptr(), sb["stats"].data_ptr(), sb["coef"].data_ptr(), 1, hp.workspace.data_ptr(), s)
+                sb1["stats"].data_ptr(), sb["stats"].data_ptr(), sb["coef"].data_ptr(), 1, 0, hp.workspace.data_ptr(), s,
+                None)
     torch.cuda.synchronize()
     assert torch.equal(coef, sb["coef"])
     assert torch.equal(sb1["stats"], sb["stats"]) and torch.equal(sb1["adv0"], sb["adv0"])

@@ -8,7 +8,8 @@ import sys
 def short(name):
     for key, lab in (("k_vocab_rows<trlx::BF16T, 13, 0", "E rows"), ("k_vocab_rows<trlx::BF16T, 9, 2", "L rows"),
                      ("k_vocab_rows", "rows(other)"), ("k_rollout_gae", "GAE tail"), ("k_rollout_loss", "loss tail"),
-                     ("k_ilql_rows", "ILQL rows"), ("k_ilql_prep", "ILQL prep"), ("k_ilql_finalize", "ILQL finalize")):
+                     ("k_ilql_rows", "ILQL rows"), ("k_ilql_prep", "ILQL prep"), ("k_ilql_finalize", "ILQL finalize"),
+                     ("k_score_moments", "score moments"), ("k_whiten_coef", "whiten coef"), ("nccl", "RCCL (side)")):
         if key in name:
             return lab
     return None
@@ -20,10 +21,14 @@ def main(path, skip=50):
     ev = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
     ev = [e for e in ev if e[0]][skip:]
     dur, gap = {}, {}
-    for i, (n, s, e) in enumerate(ev):
+    last_end = None  # the step's own stream: side-stream RCCL kernels are listed, not chained
+    for n, s, e in ev:
         dur.setdefault(n, []).append((e - s) / 1e3)
-        if i:
-            gap.setdefault(n, []).append((s - ev[i - 1][2]) / 1e3)
+        if n.endswith("(side)"):
+            continue
+        if last_end is not None:
+            gap.setdefault(n, []).append((s - last_end) / 1e3)
+        last_end = e
     med = lambda xs: sorted(xs)[len(xs) // 2]
     tot = 0.0
     for n in dur:

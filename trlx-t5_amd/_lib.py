@@ -130,7 +130,8 @@ SIGNATURES = {
     "trlx_ppo_rollout_loss_ctl": (_c_int, [_c_i64, _c_i64, _c_vp, _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
     "trlx_ppo_rollout_gae_split": (_c_int, [_c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
                                             _score_ctl_p, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
-                                            _c_vp, _c_vp, _c_int, _c_vp, _c_vp]),
+                                            _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp]),
+    "trlx_score_moments_merge": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp]),
     "trlx_ppo_whiten_coef": (_c_int, [_c_vp, _c_int, _c_vp, _c_f, _c_vp, _c_vp]),
     "trlx_ppo_loss_rows_split": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
                                           _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,

@@ -20,7 +20,31 @@ struct ScoreCtlArgs {
     const double* global_mom;  // {Σx, Σx², n} over all ranks, or NULL (local = global)
     int scale_mode;            // TRLX_SCALE_*
     float clip;                // cliprange_reward (0: no clip)
+    int lag;                   // 1: global_mom holds the PREVIOUS batch's moments (merged now; NULL: nothing
+                               // to merge yet) -- the pipelined schedule without running-std scaling
 };
+
+// RunningMoments.update's merge (modeling.py:91-102, term for term) of batch moments
+// (n, mean, biased var) into the record; also the batch statistics it returns.
+__device__ __forceinline__ void running_merge(double* st, double xn, double xm, double xv) {
+    const double delta = xm - st[TRLX_CTL_MEAN];
+    const double cnt = st[TRLX_CTL_COUNT];
+    const double tot = cnt + xn;
+    const double new_sum = xv * xn;
+    const double old_sum = st[TRLX_CTL_VAR] * cnt + delta * delta * cnt * xn / tot;
+    st[TRLX_CTL_MEAN] += delta * xn / tot;
+    st[TRLX_CTL_VAR] = (old_sum + new_sum) / tot;
+    st[TRLX_CTL_STD] = sqrt(st[TRLX_CTL_VAR] * tot / (tot - 1.0));
+    st[TRLX_CTL_COUNT] = tot;
+    st[TRLX_CTL_BATCH_MEAN] = xm;
+    st[TRLX_CTL_BATCH_STD] = sqrt(xv * xn / (xn - 1.0));
+}
+// the same from an all-reduced {Σx, Σx², n} record (get_global_statistics, biased variance)
+__device__ __forceinline__ void running_merge_global(double* st, const double* gm) {
+    const double xn = gm[2];
+    const double xm = gm[0] / xn;
+    running_merge(st, xn, xm, fmax(gm[1] - gm[0] * xm, 0.0) / xn);
+}
 
 struct KlCtlArgs {
     double* state;  // NULL: no KL update
@@ -64,28 +88,10 @@ __device__ __forceinline__ void score_ctl_block(const ScoreCtlArgs& c, const flo
         double st[TRLX_CTL_SLOTS];
 #pragma unroll
         for (int k = 0; k < TRLX_CTL_SLOTS; ++k) st[k] = c.state_in[k];
-        double xn, xm, xv;
-        if (c.global_mom) {
-            xn = c.global_mom[2];
-            xm = c.global_mom[0] / xn;
-            xv = fmax(c.global_mom[1] - c.global_mom[0] * xm, 0.0) / xn;
-        } else {
-            xn = double(n);
-            xm = lmean;
-            xv = m2 / xn;
-        }
-        // Chan merge, term for term as modeling.py:91-102
-        const double delta = xm - st[TRLX_CTL_MEAN];
-        const double cnt = st[TRLX_CTL_COUNT];
-        const double tot = cnt + xn;
-        const double new_sum = xv * xn;
-        const double old_sum = st[TRLX_CTL_VAR] * cnt + delta * delta * cnt * xn / tot;
-        st[TRLX_CTL_MEAN] += delta * xn / tot;
-        st[TRLX_CTL_VAR] = (old_sum + new_sum) / tot;
-        st[TRLX_CTL_STD] = sqrt(st[TRLX_CTL_VAR] * tot / (tot - 1.0));
-        st[TRLX_CTL_COUNT] = tot;
-        st[TRLX_CTL_BATCH_MEAN] = xm;
-        st[TRLX_CTL_BATCH_STD] = sqrt(xv * xn / (xn - 1.0));
+        if (c.global_mom)
+            running_merge_global(st, c.global_mom);  // lag: the previous batch's, all-reduced
+        else if (!c.lag)
+            running_merge(st, double(n), lmean, m2 / double(n));
         if (st[TRLX_CTL_REF_SET] == 0.0) {
             st[TRLX_CTL_REF_MEAN] = lmean;
             st[TRLX_CTL_REF_STD] = sqrt(m2 / (double(n) - 1.0));

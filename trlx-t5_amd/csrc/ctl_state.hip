@@ -50,6 +50,14 @@ __global__ __launch_bounds__(kCtlThreads) void k_score_ctl(const float* x, int n
     for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = score_transform(x[i], div, c.clip);
 }
 
+__global__ void k_moments_merge(const double* state_in, double* state_out, const double* moments) {
+    if (threadIdx.x != 0) return;
+    double st[TRLX_CTL_SLOTS];
+    for (int k = 0; k < TRLX_CTL_SLOTS; ++k) st[k] = state_in[k];
+    running_merge_global(st, moments);
+    for (int k = 0; k < TRLX_CTL_SLOTS; ++k) state_out[k] = st[k];
+}
+
 __global__ void k_kl_ctl(KlCtlArgs k, const float* approx_kl) {
     if (threadIdx.x == 0) kl_ctl_apply(k, *approx_kl);
 }
@@ -101,6 +109,13 @@ extern "C" int trlx_score_ctl_update(const void* scores, int dtype, int64_t n, c
     hipLaunchKernelGGL(k_score_ctl, dim3(1), dim3(kCtlThreads), 0, (hipStream_t)stream,
                        static_cast<const float*>(scores), int(n), c, static_cast<float*>(scores_out));
     return check_launch("k_score_ctl");
+}
+
+extern "C" int trlx_score_moments_merge(const double* state_in, double* state_out, const double* moments,
+                                        void* stream) {
+    TRLX_REQUIRE(state_in && state_out && moments, TRLX_ERR_ARG, "NULL argument to trlx_score_moments_merge");
+    hipLaunchKernelGGL(k_moments_merge, dim3(1), dim3(kWave), 0, (hipStream_t)stream, state_in, state_out, moments);
+    return check_launch("k_moments_merge");
 }
 
 extern "C" int trlx_kl_ctl_update(const trlx_kl_ctl* kl, const float* approx_kl, void* stream) {

@@ -12,6 +12,8 @@
 // contraction; the roofline is HBM bandwidth.
 #include <string>
 
+#include <hip/hip_ext.h>
+
 #include "row_tails.h"
 
 namespace trlx {
@@ -867,6 +869,8 @@ struct SplitGae {
     const double* prev_stats;
     float* prev_coef;
     int prev_unbiased;
+    int mom_lag;          // ScoreCtlArgs::lag
+    void* done_event;     // recorded by the launch's own dispatch (hipExtLaunchKernel), or NULL
 };
 
 static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
@@ -894,6 +898,11 @@ static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* 
         e.has_ctl = 1;
         e.ctl.state_in = ctl->state_in; e.ctl.state_out = ctl->state_out; e.ctl.global_mom = ctl->global_moments;
         e.ctl.scale_mode = ctl->scale_mode; e.ctl.clip = ctl->cliprange_reward;
+        if (sp && sp->mom_lag) {
+            TRLX_REQUIRE(ctl->scale_mode != TRLX_SCALE_RUNNING, TRLX_ERR_ARG,
+                         "lagged score moments cannot scale by the running std (it needs this batch's moments)");
+            e.ctl.lag = 1;
+        }
     }
     if (sp) {
         TRLX_REQUIRE(sp->adv_kl && sp->rew_kl && sp->rew_score, TRLX_ERR_ARG, "NULL split-beta GAE output");
@@ -903,7 +912,10 @@ static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* 
         e.host_beta = kl_coef;
     }
     const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
-    if (e.adv_kl)
+    if (e.adv_kl && sp->done_event)  // the side stream's ordering point rides the dispatch (no marker packet)
+        hipExtLaunchKernelGGL(k_rollout_gae<true>, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, nullptr,
+                              (hipEvent_t)sp->done_event, 0, e);
+    else if (e.adv_kl)
         hipLaunchKernelGGL(k_rollout_gae<true>, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
     else
         hipLaunchKernelGGL(k_rollout_gae<false>, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, e);
@@ -933,8 +945,9 @@ extern "C" int trlx_ppo_rollout_gae_split(int64_t B, int64_t T, const float* lp,
                                           const int64_t* lengths, const int64_t* mask, const trlx_score_ctl* ctl,
                                           float kl_coef, float gamma, float lam, float* adv0, float* adv_kl,
                                           float* rew_kl, float* rew_score, double* stats8, const double* prev_stats8,
-                                          float* prev_coef, int prev_unbiased, void* workspace, void* stream) {
-    const SplitGae sp = {adv_kl, rew_kl, rew_score, prev_stats8, prev_coef, prev_unbiased};
+                                          float* prev_coef, int prev_unbiased, int mom_lag, void* workspace,
+                                          void* stream, void* done_event) {
+    const SplitGae sp = {adv_kl, rew_kl, rew_score, prev_stats8, prev_coef, prev_unbiased, mom_lag, done_event};
     return rollout_gae_impl(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, ctl, gamma, lam,
                             nullptr, adv0, nullptr, TRLX_F32, stats8, workspace, stream, &sp);
 }

@@ -61,6 +61,19 @@ class _StreamJoin:
             self._joined = s.cuda_stream
 
 
+class _Works:
+    """Several torch.distributed async works waited together."""
+
+    __slots__ = ("_ws",)
+
+    def __init__(self, ws):
+        self._ws = ws
+
+    def wait(self):
+        for w in self._ws:
+            w.wait()
+
+
 class PPOHotPath:
     _comm_timing_events = False  # A/B knob: timing-capable events for the comm joins
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
@@ -75,6 +88,8 @@ class PPOHotPath:
         self.split_beta = bool(split_beta)
         self._sbuf = None  # split-beta buffer sets (two: the pipeline's batches k and k+1)
         self._sidx = 0     # the set the current batch uses
+        self._lag = False      # pipelined under DP without running-std scaling: score moments merged one batch late
+        self._mom_bufs = None  # lag: per-batch score moments {Σx, Σx², n, 0} (two, by batch parity)
         # comm: the boundary's RCCL helper (comm.RcclComm) for the step's all-reduces instead
         # of torch.distributed — enqueued on the step's stream (blocking schedule) or on a side
         # stream joined with fence-free events (pipelined schedule, score moments)
@@ -200,10 +215,14 @@ class PPOHotPath:
         return t
 
     # -------------------------------------------------------------- collectives
-    def _begin_step(self, scores, group, s):
+    def _begin_step(self, scores, group, s, lag=False):
         """Whether the step is distributed, and the score moments all-reduce (device controller
-        state under DP) issued so it overlaps the experience rows: (global moments, work)."""
+        state under DP) issued so it overlaps the experience rows: (global moments, work).
+        lag (pipelined, no running-std scaling): nothing here — this batch's moments ride the
+        side-stream segment issued after its GAE launch (_experience_tail)."""
         self.distributed = self.comm is not None or (dist.is_available() and dist.is_initialized())
+        if lag:
+            return None, None
         if self.comm is None:
             if self.ctl is None:
                 return None, None
@@ -231,7 +250,10 @@ class PPOHotPath:
         self._comm_ev_i = (self._comm_ev_i + 1) % len(self._comm_events)
         return ev
 
-    def _side_allreduce(self, ts, s, ready=None):
+    def _score_moments(self, scores, mom, stream):
+        _lib.call("trlx_score_moments", scores.data_ptr(), _lib.F32, scores.numel(), mom.data_ptr(), stream.cuda_stream)
+
+    def _side_allreduce(self, ts, s, ready=None, issued=False):
         """comm.allreduce_ of each tensor in `ts` (each its own collective, the same sizes as
         the blocking schedule's, so every element is summed in the same order) on a side
         stream after what `s` has queued; the returned handle's wait() orders the then-current
@@ -246,7 +268,8 @@ class PPOHotPath:
         if ev_in is None:  # `ready`: already recorded on `s` by the last launch
             ev_in = self._comm_event()
             ev_in.record(s)
-        ev_in.wait(self._comm_stream)
+        if not issued:  # issued: the side stream already waits on `ready`
+            ev_in.wait(self._comm_stream)
         for t in ts:
             self.comm.allreduce_(t, self._comm_stream)
         ev_out.record(self._comm_stream)
@@ -406,10 +429,14 @@ class PPOHotPath:
         return self.lp_old, self.ref_lp
 
     def _experience_tail(self, s, labels, old_values, scores, lengths, mask, group, g_mom, work,
-                         defer_allreduce=False, fold=None):
+                         defer_allreduce=False, fold=None, lag=False):
         """GAE tail (+ the whitening all-reduce).  Split-beta mode: trlx_ppo_rollout_gae_split
         into the current buffer set; `fold` = the previous set, whose whitening coefficients
-        this launch also emits (the pipelined schedule)."""
+        this launch also emits (the pipelined schedule).  lag: g_mom holds the PREVIOUS
+        batch's all-reduced score moments (merged into RunningMoments by this launch), and
+        this batch's moments + whitening record are all-reduced on a side-stream segment
+        that starts at this launch's own completion signal and has the next batch's loss and
+        experience rows to hide behind."""
         B, T = self.B, self.T
         if work is not None:
             work.wait()
@@ -422,10 +449,12 @@ class PPOHotPath:
             sb = self._sbuf[self._sidx]
             prev = (fold["stats"].data_ptr(), fold["coef"].data_ptr(), 0 if self.distributed else 1) \
                 if fold is not None else (None, None, 0)
+            done = self._comm_event() if (lag and self.comm is not None and not self._comm_inline) else None
             _lib.call("trlx_ppo_rollout_gae_split", *tail, self.ctl.score_ctl(g_mom) if self.ctl is not None else None,
                       self.kl_coef, float(self.cfg.gamma), float(self.cfg.lam), sb["adv0"].data_ptr(),
                       sb["adv_kl"].data_ptr(), sb["rew_kl"].data_ptr(), sb["rew_score"].data_ptr(),
-                      sb["stats"].data_ptr(), *prev, self.workspace.data_ptr(), s.cuda_stream)
+                      sb["stats"].data_ptr(), *prev, int(lag), self.workspace.data_ptr(), s.cuda_stream,
+                      done.handle if done is not None else None)
             # {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak²} (+ Σmask for the global loss normaliser)
             rec, msum = sb["stats"][:7 if self.loss_norm == "global" else 6], sb["stats"][6:7]
         else:
@@ -439,6 +468,25 @@ class PPOHotPath:
             # {Σ A, Σ A², n} (+ Σmask for the global loss normaliser): the only data-path exchange
             rec, msum = self.adv_stats[:4 if self.loss_norm == "global" else 3], self.adv_stats[3:4]
         self._ev_end("rollout_gae", s)
+        if lag and self.distributed:
+            self._ar_group, self._ar_msum = group, msum
+            mom = self._mom_bufs[self._sidx]
+            if self.comm is not None:  # one side-stream segment: moments kernel + both all-reduces
+                self._ar_unissued = None
+                if self._comm_inline:
+                    self._score_moments(scores, mom, s)
+                    self._ar_work = self._side_allreduce([rec, mom[:3]], s)
+                else:
+                    if self._comm_stream is None:
+                        self._comm_stream = torch.cuda.Stream(self.device)
+                    done.wait(self._comm_stream)
+                    self._score_moments(scores, mom, self._comm_stream)
+                    self._ar_work = self._side_allreduce([rec, mom[:3]], s, ready=done, issued=True)
+            else:
+                self._score_moments(scores, mom, s)
+                self._ar_work = _Works([dist.all_reduce(rec, dist.ReduceOp.SUM, group=group, async_op=True),
+                                        dist.all_reduce(mom[:3], dist.ReduceOp.SUM, group=group, async_op=True)])
+            return
         if self.distributed:
             self._ar_group, self._ar_msum = group, msum
             if self.comm is not None:
@@ -590,12 +638,22 @@ class PPOHotPath:
         nb = prev["buf"] ^ 1 if prev is not None else 0
         s = torch.cuda.current_stream(self.device)
         self._use_split(True, nb)
-        g_mom, work = self._begin_step(scores, group, s)  # + AR(k) on the side stream (RCCL helper)
+        # lag: without running-std scaling the rewards do not need this batch's global score
+        # moments, so RunningMoments merges them one batch late and their all-reduce leaves
+        # the front of the step (no moments launch, no side-stream hop ahead of the rows)
+        distributed = self.comm is not None or (dist.is_available() and dist.is_initialized())
+        lag = distributed and self.ctl is not None and self.ctl.scale_mode != _lib.SCALE_RUNNING
+        if lag and self._mom_bufs is None:
+            self._mom_bufs = torch.zeros((2, 4), dtype=torch.float64, device=self.device)
+        self._lag = lag
+        g_mom, work = self._begin_step(scores, group, s, lag=lag)  # + AR(k) on the side stream (RCCL, no lag)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
         self._experience_rows(logits, ref_logits, labels, s)  # + the deferred loss tail(k-1)
         self._resolve_allreduce()  # AR(k): GAE(k+1) folds batch k's whitening coefficients
+        if lag:  # batch k's all-reduced score moments (none before the first batch)
+            g_mom = self._mom_bufs[prev["buf"]] if prev is not None else None
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work, defer_allreduce=True,
-                              fold=self._sbuf[prev["buf"]] if prev is not None else None)
+                              fold=self._sbuf[prev["buf"]] if prev is not None else None, lag=lag)
         out = None
         if prev is not None:
             self._sidx, self._coef_ready = prev["buf"], True
@@ -617,6 +675,11 @@ class PPOHotPath:
         self._use_split(True, prev["buf"])
         self.lp_old, self.ref_lp = self._lp_bufs[prev["buf"]]
         self._resolve_allreduce()  # nothing left to hide it behind
+        if self._lag:  # the last batch's score moments: RunningMoments' last merge
+            st = self.ctl.state.data_ptr()
+            _lib.call("trlx_score_moments_merge", st, st, self._mom_bufs[prev["buf"]].data_ptr(),
+                      torch.cuda.current_stream(self.device).cuda_stream)
+            self._lag = False
         return self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
                                 mask=prev["mask"])
 
