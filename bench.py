@@ -309,13 +309,20 @@ def cpu_baseline(torch, T, V, seconds, dtype=None):
                       f"AdaptiveKLController: reference ops incl. autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
 
 
-def settle_and_warm(step, torch, args, dev):
+SETTLE_CHUNK = 8  # steps between the ranks' agreement on whether the settle is over (N > 1)
+
+
+def settle_and_warm(step, torch, args, dev, world=1, dist=None):
     """The W warm-up steps, then (settle) more steps until the GPU has been kept busy for
     --settle-ms.  Measured cause (tools/slowstart_probe.py, profiles/r02_slowstart.log): after
     an idle period (process start, or 1 s of sleep) this step runs 10-20 % slow for its first
     ~20-40 ms of sustained load, the read-only experience launch most (244 -> 196 us), whatever
     the buffers — a chip power/clock state, not first touch.  The queue is kept at most
-    4 steps deep (fence-free events) so the wall clock of the settle is GPU-busy time."""
+    4 steps deep (fence-free events) so the wall clock of the settle is GPU-busy time.
+    N > 1: every step carries collectives, so every rank must run the SAME number of settle
+    steps (one extra step on one rank pairs its all-reduces with the next step's of the
+    others and leaves its last one waiting forever): the ranks decide together, every
+    SETTLE_CHUNK steps, with an all-reduce of their "settled" flags (MIN: until all are)."""
     from trlx_t5_amd.timing import LaunchEvent
     t0 = time.perf_counter()
     for _ in range(args.warmup):
@@ -326,7 +333,17 @@ def settle_and_warm(step, torch, args, dev):
         s = torch.cuda.current_stream(dev)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        while (time.perf_counter() - t1) * 1e3 < args.settle_ms and extra < SETTLE_MAX_STEPS:
+        flag = torch.zeros(1, dtype=torch.int32) if world > 1 else None
+        while extra < SETTLE_MAX_STEPS:
+            if world > 1:
+                if extra % SETTLE_CHUNK == 0:
+                    flag[0] = int((time.perf_counter() - t1) * 1e3 >= args.settle_ms)
+                    f = flag.to(dev)
+                    dist.all_reduce(f, dist.ReduceOp.MIN)  # the same decision on every rank
+                    if int(f.item()):
+                        break
+            elif (time.perf_counter() - t1) * 1e3 >= args.settle_ms:
+                break
             step()
             ev = ring[extra % len(ring)]
             ev.record(s)
@@ -494,7 +511,7 @@ def main():
         # PMC bytes were collected at the config's rows per GPU
         traffic_key = None if args.global_batch else args.config + ("_fp32" if args.logits_dtype == "fp32" else "")
 
-    warm_steps, warm_ms = settle_and_warm(step, torch, args, dev)
+    warm_steps, warm_ms = settle_and_warm(step, torch, args, dev, world, dist)
     elapsed, kern_ms, samples = timed_run(step, hp, torch, dist, args, dev, world, names)
     roof = roofline(kern_ms, samples, ab, tokens, doms, elapsed, args.steps, traffic_key)
 
