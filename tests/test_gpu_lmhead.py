@@ -84,9 +84,9 @@ def test_lmhead_c2_shape_rows_and_determinism():
     torch.testing.assert_close(lp1[rows.to(DEV)].cpu().double(), want, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [3, 8])
+@pytest.mark.parametrize("variant", [3, 8, 9])
 def test_lmhead_every_variant_vs_oracle(variant):
-    """Both tile kernels (3 = 128x128 tiles, 8 = 256x256 ping-pong) on ragged shapes: N and V
+    """Every tile kernel (3 = 128x128 tiles, 8 = 256x256 ping-pong, 9 = 128x256 two per CU) on ragged shapes: N and V
     not multiples of the tile, H = 64 (one K-step: the ping-pong prologue / tail counts),
     H = 4096 (64 K-steps).  Removed variants are rejected."""
     from trlx_t5_amd import _lib

@@ -428,6 +428,162 @@ __global__ __launch_bounds__(512) void k_lmhead_pp2(LmHeadArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ two workgroups per CU
+// 128 tokens x 256 vocab per workgroup of 4 waves (2 x 2, 64 x 128 each, one wave per SIMD),
+// K in 32-deep steps through a 3-slot LDS ring (24 KB per step: 64-B rows, chunk-XOR
+// swizzled), ONE raw barrier per step, the next step's fragments read into a second register
+// set while this step's 32 MFMAs run.  74.5 KB of LDS and <= 256 VGPRs let TWO workgroups
+// share a CU, on different tiles and phases: while one runs its barrier or its per-tile
+// log-sum-exp epilogue (~1,300 VALU per wave), the other's wave on the same SIMD issues MFMAs
+// — the epilogue no longer idles the MFMA pipe as in k_lmhead_pp2, whose two waves per SIMD
+// belong to one tile.
+constexpr int kS2BK = 32;
+constexpr int kS2Stage = (128 + 256) * kS2BK * 2;  // 24 KB: A 128 rows + B 256 rows of 64 B
+constexpr int kS2Lds = 3 * kS2Stage + 2 * 128 * 8 + 128 * 4;
+typedef LmGeom<128, 256, 2, 2> LmS2;
+static_assert(LmS2::kMR == 4 && LmS2::kNR == 8, "s2 wave block is 64 x 128");
+
+// 64-B rows: physical 16-B chunk c ^ ((r >> 2) & 3) (a quarter-wave ds_read_b128 of one
+// logical chunk over 16 consecutive rows then covers all 64 banks once).
+__device__ __forceinline__ int s2_chunk(int r, int c) { return c ^ ((r >> 2) & 3); }
+__device__ __forceinline__ bf16x8_t s2_frag(const char* tile, int r, int c) {
+    return *reinterpret_cast<const bf16x8_t*>(tile + r * 64 + s2_chunk(r, c) * 16);
+}
+
+__global__ __launch_bounds__(256, 2) void k_lmhead_s2(LmHeadArgs a) {
+    typedef LmS2 G;
+    __shared__ __attribute__((aligned(16))) char smem[kS2Lds];  // ONE LDS object (glds waits)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int ntt = (a.N + G::BM - 1) / G::BM;
+    const int b = blockIdx.x;
+    const int mt = b % ntt, vt = b / ntt;
+    const int m0 = mt * G::BM, n0 = vt * G::BN;
+    float2* cmb = reinterpret_cast<float2*>(smem + 3 * kS2Stage);
+    int* lab = reinterpret_cast<int*>(smem + 3 * kS2Stage + 2 * G::BM * 8);
+    if (tid < G::BM) {  // before any LDS DMA: an ordinary load later would drain them (vmcnt(0))
+        const int m = m0 + tid;
+        lab[tid] = m < a.N ? int(a.labels[int64_t(m) * a.lb]) : -1;
+    }
+    // DMA groups: 16 rows x 64 B per wave instruction; groups 0..7 = the A tile (tokens),
+    // 8..23 = the B tile (vocab); wave w issues groups w, w+4, ..., w+20.  Lane l -> row
+    // l >> 2, physical chunk l & 3, fetching the logical chunk s2_chunk(row, physical).
+    // Buffer resources on the tile bases: the per-lane row offset (rows clamped to the last
+    // valid one) stays in VOFFSET for the whole K loop, the K step rides SOFFSET: no VALU per
+    // DMA.
+    const int rl = lane >> 2;
+    const int lc = (lane & 3) ^ ((lane >> 4) & 3);
+    const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.h + int64_t(m0) * a.ldh, 0x7ffffff0u);
+    const __amdgpu_buffer_rsrc_t rB = make_rsrc(a.w + int64_t(n0) * a.ldw, 0x7ffffff0u);
+    int voff[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int g = i * 4 + wave;
+        if (i < 2) {
+            const int r = min(g * 16 + rl, a.N - 1 - m0);
+            voff[i] = (r * int(a.ldh) + lc * 8) * 2;
+        } else {
+            const int r = min((g - 8) * 16 + rl, a.V - 1 - n0);
+            voff[i] = (r * int(a.ldw) + lc * 8) * 2;
+        }
+    }
+    auto issue = [&](int kt) {
+        char* stage = smem + (kt % 3) * kS2Stage;
+        const int soff = kt * kS2BK * 2;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                i < 2 ? rA : rB, (__attribute__((address_space(3))) void*)(stage + (i * 4 + wave) * 1024), 16,
+                voff[i], soff, 0, 0);
+    };
+    f32x4_t acc[G::kMR][G::kNR];
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fc = lane >> 4;
+    // K loop, one raw barrier per 32-deep step: retire step kt (own vmcnt, leaving kt+1 in
+    // flight; then the barrier: every wave's part landed AND every wave is done reading kt-1),
+    // issue the DMA of kt+2 into kt-1's slot, read kt's fragments, 32 MFMAs.  The second
+    // workgroup on the CU fills this wave's barrier and LDS-latency gaps.
+    const int nk = a.H / kS2BK;
+    issue(0);
+    if (nk > 1) issue(1);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk)
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) issue(kt + 2);
+        const char* At = smem + (kt % 3) * kS2Stage;
+        const char* Bt = At + G::BM * 64;
+        bf16x8_t af[G::kMR], bfr[G::kNR];
+#pragma unroll
+        for (int j = 0; j < G::kNR; ++j) bfr[j] = s2_frag(Bt, wc * G::kWCols + j * 16 + fr, fc);
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i) af[i] = s2_frag(At, wr * G::kWRows + i * 16 + fr, fc);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < G::kMR; ++i)
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();  // the labels' LDS writes (before the loop) and the stages are done with
+
+    // ---- epilogue (as k_lmhead_tiles): per token row, the tile's partial (max, Σexp) and
+    // the label logit; acc[i][j][q] at lane l = logit(token m0 + wr*64 + i*16 + (l>>4)*4 + q,
+    // vocab n0 + wc*128 + j*16 + (l&15))
+    const int cl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < G::kMR; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rt = wr * G::kWRows + i * 16 + (lane >> 4) * 4 + q;
+            float x[G::kNR];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) {
+                const int v = n0 + wc * G::kWCols + j * 16 + cl;
+                x[j] = v < a.V ? acc[i][j][q] : -INFINITY;
+                mx = fmaxf(mx, x[j]);
+            }
+            mx = row16_max(mx);
+            const float ml2e = mx == -INFINITY ? 0.f : -mx * kLog2e;
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < G::kNR; ++j) sm += exp2_fast(fmaf(x[j], kLog2e, ml2e));
+            sm = row16_sum(sm);
+            if (cl == 0) cmb[wc * G::BM + rt] = make_float2(mx, sm);
+            const int dy = lab[rt] - (n0 + wc * G::kWCols);
+            if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+                float xy = x[0];
+#pragma unroll
+                for (int j = 1; j < G::kNR; ++j) xy = (dy >> 4) == j ? x[j] : xy;
+                a.xlab[m0 + rt] = xy;
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < G::BM; t += G::kThreads) {
+        if (m0 + t >= a.N) continue;
+        float m = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < G::WN; ++c) m = fmaxf(m, cmb[c * G::BM + t].x);
+        float sm = 0.f;
+        if (m != -INFINITY) {
+#pragma unroll
+            for (int c = 0; c < G::WN; ++c) {
+                const float2 p = cmb[c * G::BM + t];
+                sm += p.x == -INFINITY ? 0.f : p.y * exp2_fast((p.x - m) * kLog2e);
+            }
+        }
+        a.part[int64_t(m0 + t) * a.nvt + vt] = make_float2(m, sm);
+    }
+}
+
 // One wave per token: merge the nvt partials (fixed order per lane, then a fixed butterfly).
 __global__ __launch_bounds__(256) void k_lmhead_combine(LmHeadArgs a, void* lp, int lp_dtype, float* lse_out) {
     const int lane = threadIdx.x & 63;
@@ -472,22 +628,25 @@ using namespace trlx;
 // persistent 3-stage form, a 4-phase ping-pong (with and without an XCD remap), persistent
 // ping-pongs and a 32-deep 4-slot ring: all slower than or tied with variant 8;
 // they were removed from the library in round 2 (git history: lmhead_rows.hip at 63d22a9).
+// Round 3: 9 = 128 x 256 tiles, two workgroups per CU (k_lmhead_s2): 0.95x variant 8 at C2's
+// H = 768 (519 vs 544 us), tied at C3, 1.23x slower at H = 4096 (its 32-deep 3-slot ring
+// keeps only ~2 K-steps of DMA in flight; profiles/r03_lmhead_s2_bench.log) -> auto for H <= 1024.
 static thread_local int g_lm_variant = 0;
-static int lm_variant(int64_t N) {
+static int lm_variant(int64_t N, int64_t H) {
     if (g_lm_variant) return g_lm_variant;
-    return N < 2048 ? 3 : 8;
+    return N < 2048 ? 3 : (H <= 1024 ? 9 : 8);
 }
-static int lm_tile_n(int64_t N) { return lm_variant(N) == 3 ? LmSmall::BN : LmBig::BN; }
+static int lm_tile_n(int64_t N, int64_t H) { return lm_variant(N, H) == 3 ? LmSmall::BN : LmBig::BN; }  // s2: 256
 static_assert(LmSmall::BN == 128 && LmBig::BN == 256, "tile widths");
 
 extern "C" int trlx_lmhead_set_variant(int v) {
-    TRLX_REQUIRE(v == 0 || v == 3 || v == 8, TRLX_ERR_ARG, "lmhead variant must be 0 (auto), 3 or 8");
+    TRLX_REQUIRE(v == 0 || v == 3 || v == 8 || v == 9, TRLX_ERR_ARG, "lmhead variant must be 0 (auto), 3, 8 or 9");
     g_lm_variant = v;
     return TRLX_OK;
 }
 
 extern "C" int64_t trlx_lmhead_workspace_bytes(int64_t N, int64_t V) {
-    const int64_t nvt = (V + lm_tile_n(N) - 1) / lm_tile_n(N);
+    const int64_t nvt = (V + lm_tile_n(N, 0) - 1) / lm_tile_n(N, 0);  // every N >= 2048 variant has BN = 256
     return N * nvt * int64_t(sizeof(float2)) + N * int64_t(sizeof(float));
 }
 
@@ -497,6 +656,14 @@ static int lm_launch_small(const LmHeadArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL((k_lmhead_tiles<LmSmall>), dim3(unsigned(ntt * a.nvt)), dim3(LmSmall::kThreads), 0, stream,
                        a);
     return check_launch("k_lmhead_tiles");
+}
+
+static int lm_launch_s2(const LmHeadArgs& a, hipStream_t stream) {
+    const int64_t ntt = (a.N + LmS2::BM - 1) / LmS2::BM;
+    TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
+    TRLX_REQUIRE(a.H % kS2BK == 0, TRLX_ERR_SHAPE, "hidden size must be a multiple of %d", kS2BK);
+    hipLaunchKernelGGL(k_lmhead_s2, dim3(unsigned(ntt * a.nvt)), dim3(256), 0, stream, a);
+    return check_launch("k_lmhead_s2");
 }
 
 static int lm_launch_pp2(const LmHeadArgs& a, hipStream_t stream) {
@@ -530,11 +697,14 @@ extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void*
     a.V = int(V);
     a.labels = labels;
     a.lb = lb;
-    const int bn = lm_tile_n(N);
+    const int bn = lm_tile_n(N, H);
     a.nvt = int((V + bn - 1) / bn);
     a.part = static_cast<float2*>(workspace);
     a.xlab = reinterpret_cast<float*>(static_cast<char*>(workspace) + N * a.nvt * int64_t(sizeof(float2)));
-    const int rc = lm_variant(N) == 8 ? lm_launch_pp2(a, (hipStream_t)stream) : lm_launch_small(a, (hipStream_t)stream);
+    const int var = lm_variant(N, H);
+    const int rc = var == 8   ? lm_launch_pp2(a, (hipStream_t)stream)
+                   : var == 9 ? lm_launch_s2(a, (hipStream_t)stream)
+                              : lm_launch_small(a, (hipStream_t)stream);
     if (rc) return rc;
     hipLaunchKernelGGL(k_lmhead_combine, dim3(unsigned((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a, lp_out,
                        lp_dtype, lse_out);
