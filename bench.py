@@ -82,10 +82,18 @@ def parse():
                    help="PPO serial schedule: run each loss tail as its own launch (default: folded into the next "
                         "step's experience rows launch, PPOHotPath(defer_tail=True); the last one is flushed inside "
                         "the timed region)")
+    p.add_argument("--split-beta", action="store_true",
+                   help="A/B: the serial schedule with the split-beta kernels the pipelined schedule runs")
+    p.add_argument("--coef-launch", action="store_true",
+                   help="A/B: split-beta loss rows read coefficients from their own launch instead of deriving them")
+    p.add_argument("--no-gae-fold", action="store_true",
+                   help="A/B: pipelined schedule with GAE(k+1) as its own launch instead of the first workgroups of "
+                        "the L rows(k) launch")
     p.add_argument("--schedule", default="auto", choices=("auto", "serial", "pipelined"),
-                   help="PPO: serial = PPOHotPath.step per batch; pipelined = pipeline_step (the next batch's "
-                        "experience rows run while this batch's whitening all-reduce is in flight; bit-identical "
-                        "results); auto = pipelined when N > 1 (there is no all-reduce at N = 1)")
+                   help="PPO: serial = PPOHotPath.step per batch (three launches: E rows, GAE, L rows); pipelined = "
+                        "pipeline_step (two launches per batch: the next batch's GAE rides the loss rows launch, "
+                        "and the next batch's experience rows run while this batch's whitening all-reduce is in "
+                        "flight; results bit-identical to step(split_beta=True)); auto = pipelined")
     p.add_argument("--dist", action="store_true",
                    help="initialise the process group even at world size 1 (rehearses the RCCL path on one GPU: "
                         "the whitening all-reduce then runs through RCCL every step)")
@@ -167,15 +175,21 @@ def dry_run(args):
             raise SystemExit(3)
 
 
-def algorithmic_bytes(V, s, masked):
+def algorithmic_bytes(V, s, masked, pipelined=False):
     """Minimum HBM bytes per response token, per launch.  Each [B,T] fp32
-    vector read or written once counts 4 B; int64 labels / mask 8 B."""
+    vector read or written once counts 4 B; int64 labels / mask 8 B.  pipelined: the
+    split-beta kernels (GAE -> A0, Ak, kl, score terms; the loss rows finish rewards and
+    returns), the GAE riding the loss rows launch."""
     mask_b = 8 if masked else 0
     exp = 2 * V * s + 8 + 2 * 4                     # K1 rows: policy + ref row, label -> lp, ref_lp
-    gae = 2 * 4 + 4 + 3 * 4 + mask_b               # lp, ref_lp, values -> rewards, adv, returns
-    loss = 2 * V * s + 8 + 4 * 6 + 2 * 4 + mask_b  # K2 rows: row + dlogits, label, 6 vectors -> lp, dv
+    if pipelined:
+        gae = 3 * 4 + 4 * 4 + mask_b               # lp, ref_lp, values -> adv0, adv_kl, rew_kl, rew_score
+        loss = 2 * V * s + 8 + 4 * 7 + 4 * 4 + mask_b + gae  # row + dlogits, label, 7 vectors -> lp, dv, rewards, returns
+    else:
+        gae = 2 * 4 + 4 + 3 * 4 + mask_b           # lp, ref_lp, values -> rewards, adv, returns
+        loss = 2 * V * s + 8 + 4 * 6 + 2 * 4 + mask_b  # K2 rows: row + dlogits, label, 6 vectors -> lp, dv
     lred = 11 * 4                                  # per-token loss record read back
-    return {"experience": exp, "loss": loss, "step": exp + gae + loss + lred}
+    return {"experience": exp, "loss": loss, "step": exp + gae + loss + lred - (gae if pipelined else 0)}
 
 
 def ilql_algorithmic_bytes(B, L, V, s, nq=2):
@@ -424,10 +438,12 @@ def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1, comm=Non
     x = make_inputs(torch, B, T, V, dev, seed=1000 + rank, masked=masked, dtype=ldt)
     cfg = P.PPOConfig()  # configs/ppo_config.yml method: adaptive KL (target 6, horizon 10000), clip 10
     ctl = None if args.host_state else P.PPOControlState.from_config(cfg, dev, n_steps=B)  # train.batch_size per process
-    pipelined = args.schedule == "pipelined" or (args.schedule == "auto" and world > 1)
+    pipelined = args.schedule in ("pipelined", "auto")
     defer = not (args.overlap_tail or args.no_defer_tail)  # pipelined too: split beta keeps its tail foldable
     hp = P.PPOHotPath(cfg, B, T, V, ldt, dev, kl_coef=0.05, ctl=ctl, overlap_tail=args.overlap_tail,
-                      loss_norm=args.loss_norm, defer_tail=defer, comm=comm)
+                      loss_norm=args.loss_norm, defer_tail=defer, comm=comm, split_beta=args.split_beta)
+    hp._fold_gae = not args.no_gae_fold
+    hp._derive_coef = not args.coef_launch
     fn = hp.pipeline_step if pipelined else hp.step  # pipelined: each call = E rows of one batch + loss of the last
 
     def step():
@@ -503,10 +519,10 @@ def main():
     else:
         ldt = torch.float32 if args.logits_dtype == "fp32" else torch.bfloat16
         hp, step, x = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world, comm)
-        schedule = "pipelined" if args.schedule == "pipelined" or (args.schedule == "auto" and world > 1) else "serial"
+        schedule = "pipelined" if args.schedule in ("pipelined", "auto") else "serial"
         names = {"experience", "loss"}
         tokens = B * T
-        ab = algorithmic_bytes(V, 4 if args.logits_dtype == "fp32" else 2, masked)
+        ab = algorithmic_bytes(V, 4 if args.logits_dtype == "fp32" else 2, masked, schedule == "pipelined")
         doms = ("experience", "loss")
         # PMC bytes were collected at the config's rows per GPU
         traffic_key = None if args.global_batch else args.config + ("_fp32" if args.logits_dtype == "fp32" else "")
@@ -528,7 +544,7 @@ def main():
         fp32_line = {"value": round(tokens * args.steps / el32, 1), "unit": "tokens/s",
                      "ms_per_step": round(el32 / args.steps * 1e3, 4), "warmup_steps_run": w32,
                      "warmup_ms": round(wms32, 1),
-                     "roofline": roofline(km32, sm32, algorithmic_bytes(V, 4, masked), tokens, doms, el32,
+                     "roofline": roofline(km32, sm32, algorithmic_bytes(V, 4, masked, schedule == "pipelined"), tokens, doms, el32,
                                           args.steps, "c2_fp32")}
         del hp32, step32, x32
         torch.cuda.empty_cache()

@@ -480,6 +480,47 @@ int trlx_ppo_loss_rows_split(const void* logits, int dtype, int64_t B, int64_t T
                              void* returns, int r_dtype, float cliprange, float cliprange_value, float vf_coef,
                              float* lp_out, void* dx, int64_t dsb, int64_t dst, float* dvalues, void* workspace,
                              void* stream);
+/* The arguments of trlx_ppo_rollout_gae_split (without the previous-batch coefficients and
+ * the done event) as one POD, for a GAE folded into another launch. */
+typedef struct {
+    int64_t B, T;
+    const float* lp;
+    const float* ref_lp;
+    const void* values;
+    int v_dtype;
+    const float* scores;              /* [B] or NULL */
+    const int64_t* lengths;           /* [B] or NULL */
+    const int64_t* mask;              /* [B,T] or NULL */
+    const trlx_score_ctl* ctl;        /* or NULL */
+    float kl_coef, gamma, lam;
+    float* adv0;
+    float* adv_kl;
+    float* rew_kl;
+    float* rew_score;
+    double* stats8;
+    int mom_lag;
+    void* workspace;                  /* trlx_ppo_workspace_bytes(B, T) */
+} trlx_gae_split_args;
+/* trlx_ppo_loss_rows_split of batch k whose rows derive the whitening coefficients
+ * themselves — coef = {mean, rsqrt(var + 1e-8), beta, 0} of A = A0 - beta*Ak from the
+ * (all-reduced) split record stats8, beta = ctl_state[TRLX_CTL_KL_COEF] or kl_coef when
+ * ctl_state is NULL (modeling.py:24-34) — so no coefficient launch sits between the record's
+ * all-reduce and the rows; row 0 stores them to `coef` for a later trlx_ppo_loss_rows_split on
+ * the same experience (the ppo_epochs pattern: beta stays the experience's).  `gae` (or NULL):
+ * the split GAE of the NEXT batch (ppo_orchestrator.py:163-167, ppo_models.py:121-139) runs as
+ * this launch's first workgroups — nothing in it depends on these rows, so the pipelined DP
+ * schedule needs no GAE launch of its own.  It must write the other split buffer set; with a
+ * ctl it reads ctl->state_in and writes ctl->state_out, and ctl_state here must not be the
+ * state_out.  done_event (a hipEvent_t or NULL) is recorded by the launch's own dispatch. */
+int trlx_ppo_loss_rows_split_gae(const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb,
+                                 int64_t st, const int64_t* labels, int64_t lb, int64_t lt, const void* old_lp,
+                                 int old_dtype, const float* adv0, const float* adv_kl, const float* rew_kl,
+                                 const float* rew_score, const double* stats8, int unbiased, const double* ctl_state,
+                                 float kl_coef, float* coef, const double* msum, const int64_t* mask,
+                                 const void* values, int v_dtype, const void* old_values, int ov_dtype,
+                                 float* rewards, void* returns, int r_dtype, float cliprange, float cliprange_value,
+                                 float vf_coef, float* lp_out, void* dx, int64_t dsb, int64_t dst, float* dvalues,
+                                 void* workspace, const trlx_gae_split_args* gae, void* stream, void* done_event);
 
 /* ---------------------------------------------------------------- RCCL stats all-reduce helper
  * SURVEY §8b "Collectives" — replaces the two dist.all_reduce calls of

@@ -158,7 +158,7 @@ def test_dp_whitening_statistics_gloo(golden, world):
 
 
 @pytest.mark.parametrize("cname,mirror", [("trlx_ilql_args", "IlqlArgs"), ("trlx_score_ctl", "ScoreCtl"),
-                                           ("trlx_kl_ctl", "KlCtl")])
+                                           ("trlx_kl_ctl", "KlCtl"), ("trlx_gae_split_args", "GaeSplitArgs")])
 def test_struct_layout_matches_header(tmp_path, cname, mirror):
     """The ctypes mirrors of the C-ABI POD structs have the C compiler's field offsets."""
     cls = getattr(_lib, mirror)

@@ -62,8 +62,18 @@ class KlCtl(ctypes.Structure):
     _fields_ = [("state", _c_vp), ("adaptive", _c_int), ("target", _c_d), ("horizon", _c_d), ("n_steps", _c_i64)]
 
 
+class GaeSplitArgs(ctypes.Structure):
+    """Mirror of trlx_gae_split_args (include/trlx_t5_amd.h)."""
+    _fields_ = [("B", _c_i64), ("T", _c_i64), ("lp", _c_vp), ("ref_lp", _c_vp), ("values", _c_vp), ("v_dtype", _c_int),
+                ("scores", _c_vp), ("lengths", _c_vp), ("mask", _c_vp), ("ctl", ctypes.POINTER(ScoreCtl)),
+                ("kl_coef", _c_f), ("gamma", _c_f), ("lam", _c_f), ("adv0", _c_vp), ("adv_kl", _c_vp),
+                ("rew_kl", _c_vp), ("rew_score", _c_vp), ("stats8", _c_vp), ("mom_lag", _c_int),
+                ("workspace", _c_vp)]
+
+
 _score_ctl_p = ctypes.POINTER(ScoreCtl)
 _kl_ctl_p = ctypes.POINTER(KlCtl)
+_gae_split_p = ctypes.POINTER(GaeSplitArgs)
 
 # name -> (restype, argtypes)   (must match include/trlx_t5_amd.h exactly)
 SIGNATURES = {
@@ -137,6 +147,11 @@ SIGNATURES = {
                                           _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                           _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_f, _c_f, _c_f,
                                           _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "trlx_ppo_loss_rows_split_gae": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
+                                              _c_i64, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,
+                                              _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp,
+                                              _c_int, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp,
+                                              _gae_split_p, _c_vp, _c_vp]),
     "trlx_comm_load": (_c_int, [ctypes.c_char_p]),
     "trlx_comm_unique_id_bytes": (_c_i64, []),
     "trlx_comm_unique_id": (_c_int, [_c_vp, _c_i64]),

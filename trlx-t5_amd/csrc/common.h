@@ -201,12 +201,16 @@ __device__ __forceinline__ bool publish_record_last(double* rec, double val, uns
 
 // Fixed-order sum of `n` records of K doubles read with sc1 loads (see above); the sums
 // end up in threads k < K (block_sum_multi layout).  `sh`: (blockDim.x/64) * K doubles.
+// `nthr` (0 = blockDim.x): the threads that take records, so a block wider than the
+// launch that normally runs this reduction sums them in the same order.
 template <int K>
-__device__ __forceinline__ double reduce_records(const double* recs, int n, double* sh) {
+__device__ __forceinline__ double reduce_records(const double* recs, int n, double* sh, int nthr = 0) {
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
+    const int stride = nthr ? nthr : int(blockDim.x);
+    #pragma unroll 1
+    for (int i = int(threadIdx.x); i < n && int(threadIdx.x) < stride; i += stride)
 #pragma unroll
         for (int k = 0; k < K; ++k)
             acc[k] += __hip_atomic_load(recs + int64_t(i) * K + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

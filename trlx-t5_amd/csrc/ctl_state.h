@@ -24,26 +24,40 @@ struct ScoreCtlArgs {
                                // to merge yet) -- the pipelined schedule without running-std scaling
 };
 
+// The RunningMoments slots of the record, as scalars (a thread holds six doubles instead of
+// the whole record: the merge also runs inside the loss rows kernel, at 64 VGPRs).
+struct RunStats {
+    double mean, var, std, count, bmean, bstd;
+    __device__ __forceinline__ void load(const double* st) {
+        mean = st[TRLX_CTL_MEAN]; var = st[TRLX_CTL_VAR]; std = st[TRLX_CTL_STD]; count = st[TRLX_CTL_COUNT];
+        bmean = st[TRLX_CTL_BATCH_MEAN]; bstd = st[TRLX_CTL_BATCH_STD];
+    }
+    __device__ __forceinline__ void store(double* st) const {
+        st[TRLX_CTL_MEAN] = mean; st[TRLX_CTL_VAR] = var; st[TRLX_CTL_STD] = std; st[TRLX_CTL_COUNT] = count;
+        st[TRLX_CTL_BATCH_MEAN] = bmean; st[TRLX_CTL_BATCH_STD] = bstd;
+    }
+};
+
 // RunningMoments.update's merge (modeling.py:91-102, term for term) of batch moments
 // (n, mean, biased var) into the record; also the batch statistics it returns.
-__device__ __forceinline__ void running_merge(double* st, double xn, double xm, double xv) {
-    const double delta = xm - st[TRLX_CTL_MEAN];
-    const double cnt = st[TRLX_CTL_COUNT];
+__device__ __forceinline__ void running_merge(RunStats& r, double xn, double xm, double xv) {
+    const double delta = xm - r.mean;
+    const double cnt = r.count;
     const double tot = cnt + xn;
     const double new_sum = xv * xn;
-    const double old_sum = st[TRLX_CTL_VAR] * cnt + delta * delta * cnt * xn / tot;
-    st[TRLX_CTL_MEAN] += delta * xn / tot;
-    st[TRLX_CTL_VAR] = (old_sum + new_sum) / tot;
-    st[TRLX_CTL_STD] = sqrt(st[TRLX_CTL_VAR] * tot / (tot - 1.0));
-    st[TRLX_CTL_COUNT] = tot;
-    st[TRLX_CTL_BATCH_MEAN] = xm;
-    st[TRLX_CTL_BATCH_STD] = sqrt(xv * xn / (xn - 1.0));
+    const double old_sum = r.var * cnt + delta * delta * cnt * xn / tot;
+    r.mean += delta * xn / tot;
+    r.var = (old_sum + new_sum) / tot;
+    r.std = sqrt(r.var * tot / (tot - 1.0));
+    r.count = tot;
+    r.bmean = xm;
+    r.bstd = sqrt(xv * xn / (xn - 1.0));
 }
 // the same from an all-reduced {Σx, Σx², n} record (get_global_statistics, biased variance)
-__device__ __forceinline__ void running_merge_global(double* st, const double* gm) {
+__device__ __forceinline__ void running_merge_global(RunStats& r, const double* gm) {
     const double xn = gm[2];
     const double xm = gm[0] / xn;
-    running_merge(st, xn, xm, fmax(gm[1] - gm[0] * xm, 0.0) / xn);
+    running_merge(r, xn, xm, fmax(gm[1] - gm[0] * xm, 0.0) / xn);
 }
 
 struct KlCtlArgs {
@@ -69,42 +83,54 @@ __device__ __forceinline__ float score_transform(float x, float div, float clip)
 // scores.mean(), scores.std() of the LOCAL batch (ppo_orchestrator.py:96-98, unbiased).
 // Outputs (all threads): the fp32 divisor for score_transform (0 = none) and beta.
 // When `writer`, thread 0 stores the advanced record to state_out.
+// nthr (0 = blockDim.x): the threads that take scores (the GAE block is 256 threads wide in
+// its arithmetic even inside a 512-thread loss rows workgroup: same partial sums, same bits).
 __device__ __forceinline__ void score_ctl_block(const ScoreCtlArgs& c, const float* scores, int n, bool writer,
-                                                float& div, float& beta) {
+                                                float& div, float& beta, int nthr = 0) {
     __shared__ double s_red[2 * (1024 / kWave)];
     __shared__ float s_out[2];
     const int nw = blockDim.x / kWave;
+    const int stride = nthr ? nthr : int(blockDim.x);
+    const int i0 = int(threadIdx.x) < stride ? int(threadIdx.x) : n;
     double s = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) s += double(scores[i]);
+    #pragma unroll 1
+    for (int i = i0; i < n; i += stride) s += double(scores[i]);
     s = block_sum_d(s, s_red);
     const double lmean = s / double(n);
     double m2 = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    #pragma unroll 1
+    for (int i = i0; i < n; i += stride) {
         const double d = double(scores[i]) - lmean;
         m2 = fma(d, d, m2);
     }
     m2 = block_sum_d(m2, s_red + nw);
     if (threadIdx.x == 0) {
-        double st[TRLX_CTL_SLOTS];
-#pragma unroll
-        for (int k = 0; k < TRLX_CTL_SLOTS; ++k) st[k] = c.state_in[k];
+        const double* si = c.state_in;
+        RunStats r;
+        r.load(si);
         if (c.global_mom)
-            running_merge_global(st, c.global_mom);  // lag: the previous batch's, all-reduced
+            running_merge_global(r, c.global_mom);  // lag: the previous batch's, all-reduced
         else if (!c.lag)
-            running_merge(st, double(n), lmean, m2 / double(n));
-        if (st[TRLX_CTL_REF_SET] == 0.0) {
-            st[TRLX_CTL_REF_MEAN] = lmean;
-            st[TRLX_CTL_REF_STD] = sqrt(m2 / (double(n) - 1.0));
-            st[TRLX_CTL_REF_SET] = 1.0;
+            running_merge(r, double(n), lmean, m2 / double(n));
+        double ref_mean = si[TRLX_CTL_REF_MEAN], ref_std = si[TRLX_CTL_REF_STD];
+        const bool set_ref = si[TRLX_CTL_REF_SET] == 0.0;
+        if (set_ref) {
+            ref_mean = lmean;
+            ref_std = sqrt(m2 / (double(n) - 1.0));
         }
         float d = 0.0f;
-        if (c.scale_mode == TRLX_SCALE_RUNNING) d = float(st[TRLX_CTL_STD]);
-        else if (c.scale_mode == TRLX_SCALE_REF) d = float(st[TRLX_CTL_REF_STD]);
+        if (c.scale_mode == TRLX_SCALE_RUNNING) d = float(r.std);
+        else if (c.scale_mode == TRLX_SCALE_REF) d = float(ref_std);
         s_out[0] = d;
-        s_out[1] = float(st[TRLX_CTL_KL_COEF]);
-        if (writer) {
-#pragma unroll
-            for (int k = 0; k < TRLX_CTL_SLOTS; ++k) c.state_out[k] = st[k];
+        s_out[1] = float(si[TRLX_CTL_KL_COEF]);
+        if (writer) {  // (state_out may alias state_in: every slot read above is read before)
+            double* so = c.state_out;
+#pragma unroll 1
+            for (int k = 0; k < TRLX_CTL_SLOTS; ++k) so[k] = si[k];  // the slots not advanced here
+            r.store(so);
+            so[TRLX_CTL_REF_MEAN] = ref_mean;
+            so[TRLX_CTL_REF_STD] = ref_std;
+            so[TRLX_CTL_REF_SET] = 1.0;
         }
     }
     __syncthreads();

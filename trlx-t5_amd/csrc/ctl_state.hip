@@ -52,10 +52,11 @@ __global__ __launch_bounds__(kCtlThreads) void k_score_ctl(const float* x, int n
 
 __global__ void k_moments_merge(const double* state_in, double* state_out, const double* moments) {
     if (threadIdx.x != 0) return;
-    double st[TRLX_CTL_SLOTS];
-    for (int k = 0; k < TRLX_CTL_SLOTS; ++k) st[k] = state_in[k];
-    running_merge_global(st, moments);
-    for (int k = 0; k < TRLX_CTL_SLOTS; ++k) state_out[k] = st[k];
+    RunStats r;
+    r.load(state_in);
+    running_merge_global(r, moments);
+    for (int k = 0; k < TRLX_CTL_SLOTS; ++k) state_out[k] = state_in[k];
+    r.store(state_out);
 }
 
 __global__ void k_kl_ctl(KlCtlArgs k, const float* approx_kl) {

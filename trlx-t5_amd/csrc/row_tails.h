@@ -75,11 +75,14 @@ struct GaeRolloutArgs {
 // the discounted KL sums.  The split record {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0}
 // gives Σ A = Σ A0 - beta Σ Ak and Σ A² = Σ A0² - 2 beta Σ A0·Ak + beta² Σ Ak² in fp64, then
 // the same {sum, sumsq, n} whitening as the unsplit path (modeling.py:24-34).
-__device__ __forceinline__ void whiten_coef_split(const double* st, int unbiased, float beta, float* coef) {
+__device__ __forceinline__ void whiten_split_coeffs(const double* st, int unbiased, float beta, float& mu, float& rstd) {
     const double b = double(beta);
     const double rec[3] = {fma(-b, st[3], st[0]), fma(b * b, st[5], fma(-2.0 * b, st[4], st[1])), st[2]};
-    float mu, rstd;
     whiten_coeffs(rec, unbiased, mu, rstd);
+}
+__device__ __forceinline__ void whiten_coef_split(const double* st, int unbiased, float beta, float* coef) {
+    float mu, rstd;
+    whiten_split_coeffs(st, unbiased, beta, mu, rstd);
     coef[0] = mu;
     coef[1] = rstd;
     coef[2] = beta;
@@ -99,12 +102,18 @@ __device__ __forceinline__ void whiten_coef_split(const double* st, int unbiased
 // waits for the previous batch's KL-controller update.  Block 0 may also emit the
 // previous batch's whitening coefficients (prev_stats -> prev_coef) with the beta the
 // state holds now.
+// One block of the GAE launch: rollouts [blk*4, blk*4 + 4) of nblk blocks.  The block is
+// kRolloutThreads (4 waves) wide in its arithmetic whatever blockDim.x is (>= 256, a multiple
+// of 64): the split GAE also runs as the first workgroups of a loss rows launch
+// (k_vocab_rows<kPpo>, trlx_ppo_loss_rows_split_gae), whose 512-thread workgroups leave waves
+// 4.. idle; their zero partials join the fixed-order sums without changing them, so both
+// forms give the same bits.  `red` holds (blockDim.x / 64) * 8 doubles.
 template <bool SPLIT>
-__global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs e) {
+__device__ __forceinline__ void gae_block(const GaeRolloutArgs& e, int blk, int nblk, double* red) {
     constexpr int NS = SPLIT ? 8 : TRLX_MOMENT_SLOTS;
-    __shared__ double red[kRolloutsPerBlock * NS];
     const int lane = threadIdx.x & (kWave - 1);
-    const int b = blockIdx.x * kRolloutsPerBlock + threadIdx.x / kWave;
+    const int wv = int(threadIdx.x / kWave);
+    const int b = wv < kRolloutsPerBlock ? blk * kRolloutsPerBlock + wv : e.B;  // waves 4..: idle
     const int T = e.T;
     double s1 = 0.0, s2 = 0.0, sm = 0.0, cnt = 0.0, sk = 0.0, sak = 0.0, skk = 0.0;
     float neg_beta = e.neg_beta, sdiv = 0.0f, sclip = 0.0f;
@@ -115,19 +124,20 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
     const bool ctl_first = e.has_ctl && e.ctl.scale_mode != TRLX_SCALE_NONE;
     if (ctl_first) {
         float beta;
-        score_ctl_block(e.ctl, e.scores, e.B, blockIdx.x == 0, sdiv, beta);
+        score_ctl_block(e.ctl, e.scores, e.B, blk == 0, sdiv, beta, kRolloutThreads);
         neg_beta = -beta;
     } else if (e.has_ctl) {
         neg_beta = -float(e.ctl.state_in[TRLX_CTL_KL_COEF]);
     }
     if (e.has_ctl) sclip = e.ctl.clip;
-    if (SPLIT && e.prev_stats && blockIdx.x == 0 && threadIdx.x == 0)
+    if (SPLIT && e.prev_stats && blk == 0 && threadIdx.x == 0)
         whiten_coef_split(e.prev_stats, e.prev_unbiased, e.has_ctl ? float(e.ctl.state_in[TRLX_CTL_KL_COEF]) : e.host_beta,
                           e.prev_coef);
     if (b < e.B) {
         const int len = e.lengths ? int(e.lengths[b]) : T;
         const float log2c = e.gl > 0.0f ? __log2f(e.gl) : -INFINITY;
         float carry = 0.0f, vcarry = 0.0f, kcarry = 0.0f;  // A (A0, Ak) and V just past the current chunk
+        #pragma unroll 1
         for (int c0 = ((T - 1) / kWave) * kWave; c0 >= 0; c0 -= kWave) {
             const int t = c0 + lane;
             const bool ok = t < T;
@@ -187,9 +197,9 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
             }
         }
     }
-    if (e.has_ctl && !ctl_first && blockIdx.x == 0) {
+    if (e.has_ctl && !ctl_first && blk == 0) {
         float d_unused, b_unused;
-        score_ctl_block(e.ctl, e.scores, e.B, true, d_unused, b_unused);
+        score_ctl_block(e.ctl, e.scores, e.B, true, d_unused, b_unused, kRolloutThreads);
     }
     double mine[NS];
     if constexpr (SPLIT) {  // {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0}
@@ -199,11 +209,18 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
         mine[0] = s1; mine[1] = s2; mine[2] = cnt; mine[3] = sm;
     }
     const double rec = block_sum_multi<NS>(mine, red);
-    if (publish_record_last<NS>(e.ws.gae_rec + blockIdx.x * NS, rec, e.ws.tickets + 0, gridDim.x)) {
+    if (publish_record_last<NS>(e.ws.gae_rec + blk * NS, rec, e.ws.tickets + 0, unsigned(nblk))) {
         __syncthreads();  // red[] reuse
-        const double tot = reduce_records<NS>(e.ws.gae_rec, gridDim.x, red);
+        const double tot = reduce_records<NS>(e.ws.gae_rec, nblk, red, kRolloutThreads);
         if (threadIdx.x < NS) e.stats[threadIdx.x] = tot;
     }
+}
+
+
+template <bool SPLIT>
+__global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs e) {
+    __shared__ double red[kRolloutsPerBlock * (SPLIT ? 8 : TRLX_MOMENT_SLOTS)];
+    gae_block<SPLIT>(e, int(blockIdx.x), int(gridDim.x), red);
 }
 
 // The split-beta whitening coefficients as a launch of its own (one thread): the serial

@@ -59,6 +59,12 @@ struct RowArgs {
     // `tail_blocks` workgroups (trlx_lsm_gather_fwd_loss_tail); row = blockIdx.x - tail_blocks
     int has_tail, tail_blocks;
     LossRolloutArgs tail;
+    // loss rows only: the NEXT batch's split GAE folded into this launch as its first
+    // `gae_blocks` workgroups (trlx_ppo_loss_rows_split_gae; no data dependency between them)
+    int has_gae, gae_blocks;
+    GaeRolloutArgs gae;
+    int lead_blocks;          // tail_blocks + gae_blocks: row = blockIdx.x - lead_blocks
+    void* done_event;         // host only: recorded by the launch's own dispatch (or NULL)
     // split-beta loss rows (trlx_ppo_loss_rows_split): adv = A0, A = A0 - beta*Ak whitened with
     // coef {mu, rstd, beta}; this launch also finishes the batch's rewards and returns
     const float* coef;
@@ -66,6 +72,14 @@ struct RowArgs {
     const float* rew_kl;
     const float* rew_score;
     float* rewards_out;
+    // split-beta rows that derive the batch's whitening coefficients themselves (no coef
+    // launch): whiten_coef_split(wstats, wunbiased, beta = wctl[KL_COEF] or wbeta), row 0
+    // storing them to coef_out for later launches on the same experience (ppo_epochs)
+    const double* wstats;
+    int wunbiased;
+    const double* wctl;
+    float wbeta;
+    float* coef_out;
 };
 
 // ------------------------------------------------------------------ shared row pieces
@@ -78,7 +92,7 @@ struct Row {
     bool y_ok;
     RowSplit<DT> s;
     __device__ __forceinline__ Row(const RowArgs& a)
-        : row(int64_t(blockIdx.x) - a.tail_blocks),
+        : row(int64_t(blockIdx.x) - a.lead_blocks),
           b(row / a.T),
           t(row - b * a.T),
           x(reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st),
@@ -94,21 +108,49 @@ struct Row {
     }
 };
 
-// Row-independent per-token scalars of the fused PPO mode.
+// Row-independent per-token scalars of the fused PPO mode.  Split-beta rows only: beta, the
+// coefficients, and the token's reward and return (ppo_orchestrator.py:164-167,
+// ppo_models.py:135), stored by split_outputs after the row.
 struct PpoScalars {
     float A, m, inv_msum, olp;
+    float beta, mu, rstd, rew, R;
 };
-// Split beta: the token's value-loss inputs {values, old_values, returns}, with the return
-// A + V (ppo_models.py:135) finished here from A = A0 - beta*Ak and stored (thread 0).
-__device__ __forceinline__ void split_value_inputs(const RowArgs& a, int64_t row, float A, float* vin) {
+// Split beta: the token's value-loss inputs {values, old_values, returns}, the return A + V
+// finished here from A = A0 - beta*Ak (R: as computed; vin[2]: as stored, which the value
+// loss sees).  No stores here: a store ahead of the row's loads would hold them back (the
+// buffer loads may not move above it).
+__device__ __forceinline__ void split_value_inputs(const RowArgs& a, int64_t row, float A, float* vin, float& R) {
     vin[0] = ld_any(a.ltok.values, a.ltok.v_dtype, row);
     vin[1] = ld_any(a.ltok.old_values, a.ltok.ov_dtype, row);
-    const float R = add_rn(A, vin[1]);
-    if (threadIdx.x == 0) st_any(const_cast<void*>(a.ltok.returns), a.ltok.r_dtype, row, R);
-    vin[2] = a.ltok.r_dtype == TRLX_BF16 ? bf2f(f2bf(R)) : R;  // the value loss sees the stored return
+    R = add_rn(A, vin[1]);
+    vin[2] = a.ltok.r_dtype == TRLX_BF16 ? bf2f(f2bf(R)) : R;
 }
-__device__ __forceinline__ float split_advantage(const RowArgs& a, int64_t row) {
-    return a.adv[row] - mul_rn(a.coef[2], a.adv_kl[row]);
+// After the row (thread 0): the split-beta token outputs — reward, return, and (row 0) the
+// whitening coefficients the rows derived, for a later loss on the same experience.
+__device__ __forceinline__ void split_outputs(const RowArgs& a, int64_t row, const PpoScalars& p) {
+    a.rewards_out[row] = p.rew;
+    st_any(const_cast<void*>(a.ltok.returns), a.ltok.r_dtype, row, p.R);
+    if (row == 0 && a.coef_out) {
+        a.coef_out[0] = p.mu;
+        a.coef_out[1] = p.rstd;
+        a.coef_out[2] = p.beta;
+        a.coef_out[3] = 0.0f;
+    }
+}
+__device__ __forceinline__ float split_advantage(const RowArgs& a, int64_t row, float beta) {
+    return a.adv[row] - mul_rn(beta, a.adv_kl[row]);
+}
+// The split-beta whitening coefficients {mu, rstd, beta} of this launch: derived from the
+// batch's record (wstats; row 0 publishes them in split_outputs) or read from a coef vector.
+__device__ __forceinline__ void split_coef(const RowArgs& a, int64_t row, float& mu, float& rstd, float& beta) {
+    if (a.wstats) {
+        beta = a.wctl ? float(a.wctl[TRLX_CTL_KL_COEF]) : a.wbeta;
+        whiten_split_coeffs(a.wstats, a.wunbiased, beta, mu, rstd);
+    } else {
+        mu = a.coef[0];
+        rstd = a.coef[1];
+        beta = a.coef[2];
+    }
 }
 
 // vin (fused loss, tokrec set): {values, old_values, returns} of the token's value loss,
@@ -117,12 +159,13 @@ __device__ __forceinline__ float split_advantage(const RowArgs& a, int64_t row) 
 __device__ __forceinline__ PpoScalars ppo_scalars(const RowArgs& a, int64_t row, float* vin, bool early) {
     PpoScalars p;
     p.A = a.adv[row];
-    if (a.coef) {  // split beta: this token's advantage, reward and return are finished here
-        const float mu = a.coef[0], rstd = a.coef[1], beta = a.coef[2];
-        const float A = split_advantage(a, row);
-        if (threadIdx.x == 0) a.rewards_out[row] = add_rn(mul_rn(-beta, a.rew_kl[row]), a.rew_score[row]);
-        p.A = mul_rn(A - mu, rstd);
-        if (early && a.tokrec) split_value_inputs(a, row, A, vin);
+    p.beta = p.mu = p.rstd = p.rew = p.R = 0.0f;
+    if (a.coef || a.wstats) {  // split beta: this token's advantage, reward and return are finished here
+        split_coef(a, row, p.mu, p.rstd, p.beta);
+        const float A = split_advantage(a, row, p.beta);
+        p.rew = add_rn(mul_rn(-p.beta, a.rew_kl[row]), a.rew_score[row]);
+        p.A = mul_rn(A - p.mu, p.rstd);
+        if (early && a.tokrec) split_value_inputs(a, row, A, vin, p.R);
     } else if (a.stats) {
         float mu, rstd;
         whiten_coeffs(a.stats, a.unbiased, mu, rstd);
@@ -187,6 +230,14 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
             return;
         }
     }
+    if constexpr (MODE == kPpo && NL > 0) {  // only the split-residency kernels host it (their VGPR
+                                             // budget is set by the row; the others run it standalone)
+        if (int(blockIdx.x) < a.gae_blocks) {  // the next batch's split GAE (block-uniform branch)
+            __shared__ double gae_red[kMaxThreads / kWave * 8];
+            gae_block<true>(a.gae, int(blockIdx.x), a.gae_blocks, gae_red);
+            return;
+        }
+    }
     typedef typename DT::elem_t E;
     constexpr int EPV = DT::kEPV;
     const int tid = threadIdx.x, nthr = blockDim.x;
@@ -194,12 +245,13 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     // Row-independent scalars first, computed by thread 0 while the row loads are in
     // flight and parked in LDS (read back after the reductions' barriers): they then
     // occupy no VGPRs beside the row.
-    __shared__ float s_ps[7];
+    __shared__ float s_ps[12];
     if (MODE == kPpo && tid == 0) {
         float vin[3];
         const PpoScalars p0 = ppo_scalars(a, r.row, vin, true);
         s_ps[0] = p0.A; s_ps[1] = p0.m; s_ps[2] = p0.inv_msum; s_ps[3] = p0.olp;
         if (a.tokrec) { s_ps[4] = vin[0]; s_ps[5] = vin[1]; s_ps[6] = vin[2]; }
+        s_ps[7] = p0.beta; s_ps[8] = p0.mu; s_ps[9] = p0.rstd; s_ps[10] = p0.rew; s_ps[11] = p0.R;
     }
 
     const int nvec = int(r.s.nvec);
@@ -434,8 +486,9 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL 
     }
     if (MODE == kPpo && tid == 0) {
         const PolicyTerms t2 = {s_tok[0], s_tok[1], s_tok[2], s_tok[3] != 0.f};
-        const PpoScalars p2 = {0.f, s_tok[4], s_tok[5], 0.f};
+        const PpoScalars p2 = {0.f, s_tok[4], s_tok[5], 0.f, s_ps[7], s_ps[8], s_ps[9], s_ps[10], s_ps[11]};
         token_record(a, r.row, t2, p2, s_ps + 4);
+        if (a.coef || a.wstats) split_outputs(a, r.row, p2);
     }
 }
 
@@ -572,11 +625,13 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
     }
     if (je >= 0) DT::store1(drow, je, je == r.y ? gy : ng * exp2_fast(fmaf(ex, kLog2e, lse_l2e)));
     if (MODE == kPpo && a.tokrec && tid == 0) {
-        if (a.coef)
-            split_value_inputs(a, r.row, split_advantage(a, r.row), vin);
+        PpoScalars p2 = ps;
+        if (a.coef || a.wstats)
+            split_value_inputs(a, r.row, split_advantage(a, r.row, ps.beta), vin, p2.R);
         else
             loss_token_inputs(a.ltok, r.row, vin);
         token_record(a, r.row, pt, ps, vin);
+        if (a.coef || a.wstats) split_outputs(a, r.row, p2);
     }
 }
 
@@ -642,20 +697,47 @@ static bool rows_same_phase(const RowArgs& a, size_t es) {
     return same_steps && ((reinterpret_cast<uintptr_t>(a.x0) ^ reinterpret_cast<uintptr_t>(a.dx)) & 15u) == 0;
 }
 
-// A folded loss tail needs one workgroup per (threads / 64) rollouts ahead of the rows.
-static dim3 rows_grid(RowArgs& a, int threads, int nten) {
-    a.tail_blocks = a.has_tail ? int((a.tail.B + threads / kWave - 1) / (threads / kWave)) : 0;
-    return dim3(unsigned(a.B * a.T + a.tail_blocks), unsigned(nten));
+// Rows launch with the launch's done event (hipExtLaunchKernel stop event) when one is set.
+#define TRLX_ROWS_LAUNCH(KERN, GRID, BLOCK, STREAM, A)                                                        \
+    do {                                                                                                     \
+        if ((A).done_event)                                                                                  \
+            hipExtLaunchKernelGGL(KERN, GRID, BLOCK, 0, STREAM, nullptr, (hipEvent_t)(A).done_event, 0, A);  \
+        else                                                                                                 \
+            hipLaunchKernelGGL(KERN, GRID, BLOCK, 0, STREAM, A);                                             \
+    } while (0)
+
+// Work folded in ahead of the rows that a kernel cannot host runs as its own launch first:
+// the loss tail (any resident kernel hosts it), the split GAE (hosted by workgroups of at
+// least kRolloutThreads threads; never by the streaming rows).
+static int lead_standalone(RowArgs& a, hipStream_t stream, bool tail, bool gae) {
+    if (tail && a.has_tail) {
+        a.has_tail = 0;
+        const unsigned nblk = unsigned((a.tail.B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
+        hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, stream, a.tail);
+        const int rc = check_launch("k_rollout_loss");
+        if (rc) return rc;
+    }
+    if (gae && a.has_gae) {
+        a.has_gae = 0;
+        const unsigned nblk = unsigned((a.gae.B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
+        hipLaunchKernelGGL(k_rollout_gae<true>, dim3(nblk), dim3(kRolloutThreads), 0, stream, a.gae);
+        const int rc = check_launch("k_rollout_gae");
+        if (rc) return rc;
+    }
+    return TRLX_OK;
 }
 
-// Kernels that cannot host the folded loss tail run it as its own launch first.
-static int tail_standalone(RowArgs& a, hipStream_t stream) {
-    if (!a.has_tail) return TRLX_OK;
-    a.has_tail = 0;
-    a.tail_blocks = 0;
-    const unsigned nblk = unsigned((a.tail.B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
-    hipLaunchKernelGGL(k_rollout_loss, dim3(nblk), dim3(kRolloutThreads), 0, stream, a.tail);
-    return check_launch("k_rollout_loss");
+// Leading workgroups of a rows launch of `threads`-wide workgroups: a folded loss tail needs
+// one per (threads / 64) rollouts, a folded GAE one per 4 rollouts (split-residency kernels
+// only: `split`).
+static int rows_grid(RowArgs& a, int threads, int nten, hipStream_t stream, dim3& grid, bool split) {
+    const int rc = lead_standalone(a, stream, false, !split || threads < kRolloutThreads);
+    if (rc) return rc;
+    a.tail_blocks = a.has_tail ? int((a.tail.B + threads / kWave - 1) / (threads / kWave)) : 0;
+    a.gae_blocks = a.has_gae ? int((a.gae.B + kRolloutsPerBlock - 1) / kRolloutsPerBlock) : 0;
+    a.lead_blocks = a.tail_blocks + a.gae_blocks;
+    grid = dim3(unsigned(a.B * a.T + a.lead_blocks), unsigned(nten));
+    return TRLX_OK;
 }
 
 template <int MODE, class DT>
@@ -670,11 +752,13 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
         const int64_t nvec = a.V / 8 + 1 + (kLineVecs - 1);
         const bool want = g_split_lds == 2 || (g_split_lds == 0 && MODE != kFwd);
         if (want && !g_row_variant && !g_resident_threads && nvec > 512 * 8 && nvec <= 512 * (9 + 4)) {
-            const dim3 grid = rows_grid(a, 512, nten);
+            dim3 grid;
+            const int rc = rows_grid(a, 512, nten, stream, grid, true);
+            if (rc) return rc;
             if (MODE == kFwd || rows_same_phase(a, 2))
-                hipLaunchKernelGGL((k_vocab_rows<DT, 9, MODE, true, false, 4, 6>), grid, dim3(512), 0, stream, a);
+                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 9, MODE, true, false, 4, 6>), grid, dim3(512), stream, a);
             else
-                hipLaunchKernelGGL((k_vocab_rows<DT, 9, MODE, false, false, 4, 6>), grid, dim3(512), 0, stream, a);
+                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 9, MODE, false, false, 4, 6>), grid, dim3(512), stream, a);
             return check_launch("k_vocab_rows (split LDS, bf16)");
         }
         // mid-length bf16 rows (V 16k-32k, T5/UL2's 32128) in the loss / backward: the last
@@ -687,11 +771,13 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
         const int sm = g_split_mid ? g_split_mid : (grad_bytes > kSC1Bytes && !g_store_pol ? 1 : 3);
         if (MODE != kFwd && sm > 1 && g_split_lds != 1 && !g_row_variant && !g_resident_threads &&
             nvec > 512 * 4 && nvec <= 512 * 8 && rows_same_phase(a, 2)) {
-            const dim3 grid = rows_grid(a, 512, nten);
+            dim3 grid;
+            const int rc = rows_grid(a, 512, nten, stream, grid, true);
+            if (rc) return rc;
             if (sm == 3)
-                hipLaunchKernelGGL((k_vocab_rows<DT, 6, MODE, true, false, 2, 8>), grid, dim3(512), 0, stream, a);
+                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 6, MODE, true, false, 2, 8>), grid, dim3(512), stream, a);
             else
-                hipLaunchKernelGGL((k_vocab_rows<DT, 5, MODE, true, false, 3, 8>), grid, dim3(512), 0, stream, a);
+                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 5, MODE, true, false, 3, 8>), grid, dim3(512), stream, a);
             return check_launch("k_vocab_rows (split LDS, mid bf16)");
         }
     }
@@ -700,11 +786,13 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
         const int64_t nvec = a.V / 4 + 1 + (kLineVecs - 1);
         const bool want = g_split_lds == 2 || (g_split_lds == 0 && MODE != kFwd);
         if (want && !g_row_variant && !g_resident_threads && nvec > 512 * 16 && nvec <= 512 * (21 + 4)) {
-            const dim3 grid = rows_grid(a, 512, nten);
+            dim3 grid;
+            const int rc = rows_grid(a, 512, nten, stream, grid, true);
+            if (rc) return rc;
             if (MODE == kFwd || rows_same_phase(a, 4))
-                hipLaunchKernelGGL((k_vocab_rows<DT, 21, MODE, true, false, 4>), grid, dim3(512), 0, stream, a);
+                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 21, MODE, true, false, 4>), grid, dim3(512), stream, a);
             else
-                hipLaunchKernelGGL((k_vocab_rows<DT, 21, MODE, false, false, 4>), grid, dim3(512), 0, stream, a);
+                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 21, MODE, false, false, 4>), grid, dim3(512), stream, a);
             return check_launch("k_vocab_rows (split LDS)");
         }
     }
@@ -712,31 +800,34 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     const Geometry g = pick_geometry(a.V, sizeof(typename DT::elem_t), MODE != kFwd || g_resident_threads > 0);
     const int variant = g_row_variant ? g_row_variant : (g.nv > 0 ? 1 : 2);
     if (variant == 2 || g.nv == 0) {
-        const int rc = tail_standalone(a, stream);
+        const int rc = lead_standalone(a, stream, true, true);
         if (rc) return rc;
+        a.tail_blocks = a.gae_blocks = a.lead_blocks = 0;
         const dim3 grid(unsigned(a.B * a.T), unsigned(nten));
         const int thr = g_stream_threads ? g_stream_threads : kStreamMaxThreads;
         const int unroll = g_stream_unroll ? g_stream_unroll : 4;
         if (unroll == 8)
-            hipLaunchKernelGGL((k_vocab_rows_stream<DT, 8, MODE>), grid, dim3(thr), 0, stream, a);
+            TRLX_ROWS_LAUNCH((k_vocab_rows_stream<DT, 8, MODE>), grid, dim3(thr), stream, a);
         else if (unroll == 2)
-            hipLaunchKernelGGL((k_vocab_rows_stream<DT, 2, MODE>), grid, dim3(thr), 0, stream, a);
+            TRLX_ROWS_LAUNCH((k_vocab_rows_stream<DT, 2, MODE>), grid, dim3(thr), stream, a);
         else
-            hipLaunchKernelGGL((k_vocab_rows_stream<DT, 4, MODE>), grid, dim3(thr), 0, stream, a);
+            TRLX_ROWS_LAUNCH((k_vocab_rows_stream<DT, 4, MODE>), grid, dim3(thr), stream, a);
         return check_launch("k_vocab_rows_stream");
     }
     const dim3 block(g.threads);
-    const dim3 grid = rows_grid(a, g.threads, nten);
+    dim3 grid;
+    const int rc = rows_grid(a, g.threads, nten, stream, grid, false);
+    if (rc) return rc;
     const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
     const bool lb512 = g.threads <= 512 && g_resident_lb512;
 #define TRLX_RESIDENT_CASE(N)                                                                          \
     case N:                                                                                           \
         if (same && lb512)                                                                            \
-            hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE, true, true>), grid, block, 0, stream, a);   \
+            TRLX_ROWS_LAUNCH((k_vocab_rows<DT, N, MODE, true, true>), grid, block, stream, a);   \
         else if (same)                                                                                \
-            hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE, true, false>), grid, block, 0, stream, a);  \
+            TRLX_ROWS_LAUNCH((k_vocab_rows<DT, N, MODE, true, false>), grid, block, stream, a);  \
         else                                                                                          \
-            hipLaunchKernelGGL((k_vocab_rows<DT, N, MODE, MODE == kFwd, false>), grid, block, 0, stream, a); \
+            TRLX_ROWS_LAUNCH((k_vocab_rows<DT, N, MODE, MODE == kFwd, false>), grid, block, stream, a); \
         break;
     switch (g.nv) {
         TRLX_RESIDENT_CASE(1) TRLX_RESIDENT_CASE(2) TRLX_RESIDENT_CASE(3) TRLX_RESIDENT_CASE(4)
@@ -818,7 +909,7 @@ extern "C" int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int
     int rc = fill_loss_tail(&a.tail, tail_B, tail_T, tail_stats, vf_coef, loss, loss_stats, workspace, kl);
     if (rc) return rc;
     a.has_tail = 1;
-    if (B * T == 0 && B >= 0 && T >= 0) return tail_standalone(a, (hipStream_t)stream);
+    if (B * T == 0 && B >= 0 && T >= 0) return lead_standalone(a, (hipStream_t)stream, true, false);
     rc = check_rows(a, dtype);
     if (rc) return rc;
     TRLX_REQUIRE(out_lp0 && (!x1 || out_lp1), TRLX_ERR_ARG, "NULL logprob output");
@@ -873,16 +964,15 @@ struct SplitGae {
     void* done_event;     // recorded by the launch's own dispatch (hipExtLaunchKernel), or NULL
 };
 
-static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
-                            int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
-                            float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
-                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream,
-                            const SplitGae* sp = nullptr) {
+static int fill_gae(GaeRolloutArgs& e, int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                    int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask, float kl_coef,
+                    const trlx_score_ctl* ctl, float gamma, float lam, float* rewards, float* adv_raw, void* ret,
+                    int ret_dtype, double* stats, void* workspace, const SplitGae* sp) {
     TRLX_REQUIRE(B > 0 && T > 0 && B * T < (1LL << 31), TRLX_ERR_SHAPE, "bad rollout batch %lld x %lld",
                  (long long)B, (long long)T);
     TRLX_REQUIRE(lp && ref_lp && values && adv_raw && stats && workspace && (sp || (rewards && ret)), TRLX_ERR_ARG,
                  "NULL argument to trlx_ppo_rollout_gae");
-    GaeRolloutArgs e = {};
+    e = {};
     carve_workspace(workspace, B, T, &e.ws);
     e.B = int(B); e.T = int(T); e.lp = lp; e.ref_lp = ref_lp; e.values = values; e.v_dtype = v_dtype;
     e.scores = scores; e.lengths = lengths; e.mask = mask; e.neg_beta = -kl_coef; e.gamma = gamma;
@@ -911,6 +1001,18 @@ static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* 
         e.prev_stats = sp->prev_stats; e.prev_coef = sp->prev_coef; e.prev_unbiased = sp->prev_unbiased;
         e.host_beta = kl_coef;
     }
+    return TRLX_OK;
+}
+
+static int rollout_gae_impl(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
+                            int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
+                            float kl_coef, const trlx_score_ctl* ctl, float gamma, float lam, float* rewards,
+                            float* adv_raw, void* ret, int ret_dtype, double* stats, void* workspace, void* stream,
+                            const SplitGae* sp = nullptr) {
+    GaeRolloutArgs e;
+    const int rc = fill_gae(e, B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, ctl, gamma, lam,
+                            rewards, adv_raw, ret, ret_dtype, stats, workspace, sp);
+    if (rc) return rc;
     const unsigned nblk = unsigned((B + kRolloutsPerBlock - 1) / kRolloutsPerBlock);
     if (e.adv_kl && sp->done_event)  // the side stream's ordering point rides the dispatch (no marker packet)
         hipExtLaunchKernelGGL(k_rollout_gae<true>, dim3(nblk), dim3(kRolloutThreads), 0, (hipStream_t)stream, nullptr,
@@ -1028,6 +1130,55 @@ extern "C" int trlx_ppo_loss_rows_split(const void* logits, int dtype, int64_t B
     a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
     a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
     a.ltok.dv = dvalues;
+    return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
+}
+
+extern "C" int trlx_ppo_loss_rows_split_gae(
+    const void* logits, int dtype, int64_t B, int64_t T, int64_t V, int64_t sb, int64_t st, const int64_t* labels,
+    int64_t lb, int64_t lt, const void* old_lp, int old_dtype, const float* adv0, const float* adv_kl,
+    const float* rew_kl, const float* rew_score, const double* stats8, int unbiased, const double* ctl_state,
+    float kl_coef, float* coef, const double* msum, const int64_t* mask, const void* values, int v_dtype,
+    const void* old_values, int ov_dtype, float* rewards, void* returns, int r_dtype, float cliprange,
+    float cliprange_value, float vf_coef, float* lp_out, void* dx, int64_t dsb, int64_t dst, float* dvalues,
+    void* workspace, const trlx_gae_split_args* gae, void* stream, void* done_event) {
+    RowArgs a = {};
+    a.x0 = logits; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st; a.labels = labels; a.lb = lb; a.lt = lt;
+    a.old_lp = old_lp; a.old_dtype = old_dtype; a.adv = adv0; a.adv_kl = adv_kl; a.rew_kl = rew_kl;
+    a.rew_score = rew_score; a.rewards_out = rewards;
+    a.wstats = stats8; a.wunbiased = unbiased; a.wctl = ctl_state; a.wbeta = kl_coef; a.coef_out = coef;
+    a.mask = mask; a.msum = msum; a.msum_host = double(B * T); a.cliprange = cliprange;
+    a.lp_out = lp_out; a.dx = dx; a.dsb = dsb; a.dst = dst;
+    a.done_event = done_event;
+    int rc = check_rows(a, dtype);
+    if (rc) return rc;
+    TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
+    TRLX_REQUIRE(old_lp && adv0 && adv_kl && rew_kl && rew_score && stats8 && rewards && values && old_values &&
+                 returns && lp_out && dx && dvalues && workspace, TRLX_ERR_ARG,
+                 "NULL argument to trlx_ppo_loss_rows_split_gae");
+    TRLX_REQUIRE(r_dtype == TRLX_F32 || r_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "returns dtype %d", r_dtype);
+    Workspace ws;
+    carve_workspace(workspace, B, T, &ws);
+    a.tokrec = ws.tokrec;
+    a.ltok.values = values; a.ltok.v_dtype = v_dtype; a.ltok.old_values = old_values; a.ltok.ov_dtype = ov_dtype;
+    a.ltok.returns = returns; a.ltok.r_dtype = r_dtype; a.ltok.cv = cliprange_value; a.ltok.vf_coef = vf_coef;
+    a.ltok.dv = dvalues;
+    if (gae) {
+        // the GAE's tickets / block records and the rows' token records share a workspace
+        // only when it is carved for the same batch shape
+        TRLX_REQUIRE(gae->workspace != workspace || (gae->B == B && gae->T == T), TRLX_ERR_ARG,
+                     "folded GAE of a %lld x %lld batch cannot share the %lld x %lld loss workspace",
+                     (long long)gae->B, (long long)gae->T, (long long)B, (long long)T);
+        TRLX_REQUIRE(gae->stats8 != stats8 && gae->adv0 != adv0 && gae->adv_kl != adv_kl, TRLX_ERR_ARG,
+                     "the folded GAE must write the other split buffer set (it runs beside these rows)");
+        const SplitGae sp = {gae->adv_kl, gae->rew_kl, gae->rew_score, nullptr, nullptr, 0, gae->mom_lag, nullptr};
+        rc = fill_gae(a.gae, gae->B, gae->T, gae->lp, gae->ref_lp, gae->values, gae->v_dtype, gae->scores,
+                      gae->lengths, gae->mask, gae->kl_coef, gae->ctl, gae->gamma, gae->lam, nullptr, gae->adv0,
+                      nullptr, TRLX_F32, gae->stats8, gae->workspace, &sp);
+        if (rc) return rc;
+        TRLX_REQUIRE(!gae->ctl || (ctl_state != gae->ctl->state_out), TRLX_ERR_ARG,
+                     "the rows read beta from the state the folded GAE writes (pass its state_in)");
+        a.has_gae = 1;
+    }
     return launch_rows<kPpo>(a, dtype, 1, (hipStream_t)stream);
 }
 

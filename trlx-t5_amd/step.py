@@ -29,6 +29,8 @@ rank-local unless loss_norm="global" (Σmask then rides the whitening all-reduce
 """
 from typing import Optional
 
+import ctypes
+
 import torch
 import torch.distributed as dist
 
@@ -76,6 +78,8 @@ class _Works:
 
 class PPOHotPath:
     _comm_timing_events = False  # A/B knob: timing-capable events for the comm joins
+    _fold_gae = True  # A/B knob: pipeline_step runs GAE(k+1) inside the L rows(k) launch (else its own launch)
+    _derive_coef = True  # A/B knob: split loss rows derive the whitening coefficients (else a coefficient launch)
     def __init__(self, cfg: PPOConfig, B: int, T: int, V: int, logits_dtype: torch.dtype,
                  device, kl_coef: float, value_dtype: torch.dtype = torch.float32,
                  ctl: Optional[PPOControlState] = None, overlap_tail: bool = False, loss_norm: str = "rank",
@@ -429,35 +433,45 @@ class PPOHotPath:
         return self.lp_old, self.ref_lp
 
     def _experience_tail(self, s, labels, old_values, scores, lengths, mask, group, g_mom, work,
-                         defer_allreduce=False, fold=None, lag=False):
+                         defer_allreduce=False, lag=False, launch=True):
         """GAE tail (+ the whitening all-reduce).  Split-beta mode: trlx_ppo_rollout_gae_split
-        into the current buffer set; `fold` = the previous set, whose whitening coefficients
-        this launch also emits (the pipelined schedule).  lag: g_mom holds the PREVIOUS
-        batch's all-reduced score moments (merged into RunningMoments by this launch), and
-        this batch's moments + whitening record are all-reduced on a side-stream segment
-        that starts at this launch's own completion signal and has the next batch's loss and
-        experience rows to hide behind."""
+        into the current buffer set.  lag: g_mom holds the PREVIOUS batch's all-reduced score
+        moments (merged into RunningMoments by this launch), and this batch's moments +
+        whitening record are all-reduced on a side-stream segment that starts at this launch's
+        own completion signal and has the next batch's loss and experience rows to hide behind.
+        launch=False (split mode, the pipelined schedule): the GAE's arguments are returned
+        instead of launched — the caller folds the GAE into the previous batch's loss rows
+        launch (trlx_ppo_loss_rows_split_gae) and then calls _gae_done() with them."""
         B, T = self.B, self.T
         if work is not None:
             work.wait()
         if self.tail_done is not None:  # previous loss tail: reads Σmask + token records, updates beta
             self.tail_done.wait(s)
-        self._ev("rollout_gae", s)
         tail = (B, T, self.lp_old.data_ptr(), self.ref_lp.data_ptr(), old_values.data_ptr(),
                 _lib.dtype_code(old_values), _lib.ptr(scores), _lib.ptr(lengths), _lib.ptr(mask))
         if self._split_mode:
             sb = self._sbuf[self._sidx]
-            prev = (fold["stats"].data_ptr(), fold["coef"].data_ptr(), 0 if self.distributed else 1) \
-                if fold is not None else (None, None, 0)
-            done = self._comm_event() if (lag and self.comm is not None and not self._comm_inline) else None
-            _lib.call("trlx_ppo_rollout_gae_split", *tail, self.ctl.score_ctl(g_mom) if self.ctl is not None else None,
-                      self.kl_coef, float(self.cfg.gamma), float(self.cfg.lam), sb["adv0"].data_ptr(),
-                      sb["adv_kl"].data_ptr(), sb["rew_kl"].data_ptr(), sb["rew_score"].data_ptr(),
-                      sb["stats"].data_ptr(), *prev, int(lag), self.workspace.data_ptr(), s.cuda_stream,
-                      done.handle if done is not None else None)
+            done = self._comm_event() if (lag and self.distributed and self.comm is not None
+                                          and not self._comm_inline) else None
+            beta_state = self.ctl.state.data_ptr() if self.ctl is not None else None  # the GAE's state_in
+            ctl = self.ctl.score_ctl(g_mom) if self.ctl is not None else None
             # {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak²} (+ Σmask for the global loss normaliser)
-            rec, msum = sb["stats"][:7 if self.loss_norm == "global" else 6], sb["stats"][6:7]
+            gd = dict(rec=sb["stats"][:7 if self.loss_norm == "global" else 6], msum=sb["stats"][6:7], done=done,
+                      scores=scores, group=group, lag=lag, defer=defer_allreduce, beta_state=beta_state, ctl=ctl)
+            if not launch:
+                gd["args"] = _lib.GaeSplitArgs(
+                    *tail, ctypes.pointer(ctl) if ctl is not None else None, self.kl_coef, float(self.cfg.gamma),
+                    float(self.cfg.lam), sb["adv0"].data_ptr(), sb["adv_kl"].data_ptr(), sb["rew_kl"].data_ptr(),
+                    sb["rew_score"].data_ptr(), sb["stats"].data_ptr(), int(lag), self.workspace.data_ptr())
+                return gd
+            self._ev("rollout_gae", s)
+            _lib.call("trlx_ppo_rollout_gae_split", *tail, ctl, self.kl_coef, float(self.cfg.gamma),
+                      float(self.cfg.lam), sb["adv0"].data_ptr(), sb["adv_kl"].data_ptr(), sb["rew_kl"].data_ptr(),
+                      sb["rew_score"].data_ptr(), sb["stats"].data_ptr(), None, None, 0, int(lag),
+                      self.workspace.data_ptr(), s.cuda_stream, done.handle if done is not None else None)
+            self._ev_end("rollout_gae", s)
         else:
+            self._ev("rollout_gae", s)
             outs = (float(self.cfg.gamma), float(self.cfg.lam), self.rewards.data_ptr(), self.adv_raw.data_ptr(),
                     self.returns.data_ptr(), _lib.dtype_code(self.returns), self.adv_stats.data_ptr(),
                     self.workspace.data_ptr(), s.cuda_stream)
@@ -465,12 +479,21 @@ class PPOHotPath:
                 _lib.call("trlx_ppo_rollout_gae_ctl", *tail, self.ctl.score_ctl(g_mom), *outs)
             else:
                 _lib.call("trlx_ppo_rollout_gae", *tail, self.kl_coef, *outs)
+            self._ev_end("rollout_gae", s)
             # {Σ A, Σ A², n} (+ Σmask for the global loss normaliser): the only data-path exchange
-            rec, msum = self.adv_stats[:4 if self.loss_norm == "global" else 3], self.adv_stats[3:4]
-        self._ev_end("rollout_gae", s)
-        if lag and self.distributed:
+            gd = dict(rec=self.adv_stats[:4 if self.loss_norm == "global" else 3], msum=self.adv_stats[3:4],
+                      done=None, scores=scores, group=group, lag=lag, defer=defer_allreduce)
+        self._gae_done(gd, s)
+
+    def _gae_done(self, gd, s):
+        """After the GAE launch (its own, or the loss rows launch it rode): the whitening
+        record's all-reduce — blocking, deferred to the next _begin_step, or (lag) on the
+        side-stream segment behind the launch's done event."""
+        rec, msum, group = gd["rec"], gd["msum"], gd["group"]
+        if gd["lag"] and self.distributed:
             self._ar_group, self._ar_msum = group, msum
             mom = self._mom_bufs[self._sidx]
+            scores, done = gd["scores"], gd["done"]
             if self.comm is not None:  # one side-stream segment: moments kernel + both all-reduces
                 self._ar_unissued = None
                 if self._comm_inline:
@@ -490,14 +513,14 @@ class PPOHotPath:
         if self.distributed:
             self._ar_group, self._ar_msum = group, msum
             if self.comm is not None:
-                if defer_allreduce:  # issued with the next batch's score moments (_begin_step)
+                if gd["defer"]:  # issued with the next batch's score moments (_begin_step)
                     self._ar_unissued, self._ar_work = rec, None
                 else:  # on the step's own stream: ordered with no join at all
                     self.comm.allreduce_(rec, s)
                     self._ar_work = _StreamJoin(None, self.device)
             else:
                 self._ar_work = dist.all_reduce(rec, dist.ReduceOp.SUM, group=group, async_op=True)
-            if not defer_allreduce:
+            if not gd["defer"]:
                 self._resolve_allreduce()
 
     def _resolve_allreduce(self):
@@ -515,8 +538,10 @@ class PPOHotPath:
             self._ar_msum.div_(world)
 
     # -------------------------------------------------------------- K2
-    def policy_loss(self, new_logits, labels, values, old_values, mask=None):
-        """K2: fused logprob + PPO grads + dlogits, value loss, loss + stats."""
+    def policy_loss(self, new_logits, labels, values, old_values, mask=None, _fold=None):
+        """K2: fused logprob + PPO grads + dlogits, value loss, loss + stats.  (_fold: the
+        pipelined schedule's next-batch split GAE, _experience_tail(launch=False), run as the
+        first workgroups of this launch; _gae_done() follows.)"""
         self._check(new_logits)
         B, T, V = self.B, self.T, self.V
         labels = self._int64(labels, (B, T), "labels")
@@ -538,27 +563,43 @@ class PPOHotPath:
                 _lib.F32)
         grads = (float(self.cfg.cliprange), float(self.cfg.cliprange_value), float(self.cfg.vf_coef),
                  self.lp_new.data_ptr(), dx.data_ptr(), dx.stride(0), dx.stride(1), self.dvalues.data_ptr(),
-                 self.workspace.data_ptr(), s.cuda_stream)
+                 self.workspace.data_ptr())
+        if _fold is not None and not (self._split_mode and not self._coef_ready):
+            raise RuntimeError("a folded GAE rides the first split-beta loss launch of an experience")
         if self._split_mode:
             sb = self._sbuf[self._sidx]
-            if not self._coef_ready:  # not folded into a GAE launch: the coefficients as their own launch
+            split = (sb["adv0"].data_ptr(), sb["adv_kl"].data_ptr(), sb["rew_kl"].data_ptr(),
+                     sb["rew_score"].data_ptr())
+            vals = (sb["stats"].data_ptr() + 6 * 8, _lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values),
+                    old_values.data_ptr(), _lib.dtype_code(old_values), self.rewards.data_ptr(),
+                    self.returns.data_ptr(), _lib.dtype_code(self.returns))
+            self._ev("loss", s)
+            if not self._coef_ready and not self._derive_coef and _fold is None:  # A/B: the coefficient launch
                 _lib.call("trlx_ppo_whiten_coef", sb["stats"].data_ptr(), 0 if self.distributed else 1,
                           self.ctl.state.data_ptr() if self.ctl is not None else None, self.kl_coef,
                           sb["coef"].data_ptr(), s.cuda_stream)
-            self._coef_ready = True  # a second loss on this experience (ppo_epochs) reuses them
-            self._ev("loss", s)
-            _lib.call("trlx_ppo_loss_rows_split", *rows, sb["adv0"].data_ptr(), sb["adv_kl"].data_ptr(),
-                      sb["rew_kl"].data_ptr(), sb["rew_score"].data_ptr(), sb["coef"].data_ptr(),
-                      sb["stats"].data_ptr() + 6 * 8, _lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values),
-                      old_values.data_ptr(), _lib.dtype_code(old_values), self.rewards.data_ptr(),
-                      self.returns.data_ptr(), _lib.dtype_code(self.returns), *grads)
+                self._coef_ready = True
+            if self._coef_ready:  # a second loss on this experience (ppo_epochs): the stored coefficients
+                _lib.call("trlx_ppo_loss_rows_split", *rows, *split, sb["coef"].data_ptr(), *vals, *grads,
+                          s.cuda_stream)
+            else:  # the rows derive the whitening coefficients (beta: the state the GAE read) and store them
+                if _fold is not None:
+                    beta_state = _fold["beta_state"]
+                else:
+                    beta_state = self.ctl.state.data_ptr() if self.ctl is not None else None
+                done = _fold["done"] if _fold is not None else None
+                _lib.call("trlx_ppo_loss_rows_split_gae", *rows, *split, sb["stats"].data_ptr(),
+                          0 if self.distributed else 1, beta_state, self.kl_coef, sb["coef"].data_ptr(), *vals,
+                          *grads, ctypes.byref(_fold["args"]) if _fold is not None else None, s.cuda_stream,
+                          done.handle if done is not None else None)
+                self._coef_ready = True
             tail_stats = sb["stats"].data_ptr() + 3 * 8  # the tail reads Σmask at stats[3]
         else:
             self._ev("loss", s)
             _lib.call("trlx_ppo_loss_rows", *rows, self.adv_raw.data_ptr(), self.adv_stats.data_ptr(),
                       0 if self.distributed else 1, _lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values),
                       old_values.data_ptr(), _lib.dtype_code(old_values), self.returns.data_ptr(),
-                      _lib.dtype_code(self.returns), *grads)
+                      _lib.dtype_code(self.returns), *grads, s.cuda_stream)
             tail_stats = self.adv_stats.data_ptr()
         self._ev_end("loss", s)
         ts = s
@@ -604,23 +645,26 @@ class PPOHotPath:
     # -------------------------------------------------------------- pipelined schedule (DP > 1)
     def pipeline_step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
                       lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None):
-        """Software-pipelined step for data parallelism.  Per call (batch k+1):
+        """Software-pipelined step (the data-parallel schedule; bit-identical to step() with
+        split_beta=True at any world size).  Per call (batch k+1), two launches:
 
             E rows(k+1) [+ loss tail(k-1)] | [AR(k) in flight beside them]
-              -> join AR(k) -> GAE(k+1) [+ whitening coefficients of batch k] -> AR(k+1) async
-              -> L rows(k)  [loss tail(k) deferred into the next E launch]
+              -> join AR(k) -> L rows(k) [+ GAE(k+1) as the launch's first workgroups] -> AR(k+1) async
+                                         [tail(k) deferred into the next E launch]
 
         Split beta (trlx_ppo_rollout_gae_split): the reward r = score - beta*kl enters GAE
-        linearly, so GAE(k+1) runs before the KL-controller update of loss tail(k) and the
-        loss rows apply beta (A = A0 - beta*Ak, rewards, returns).  Every loss sees the beta
-        the serial schedule would give it, so losses, stats, gradients and controller state
-        are bit-identical to step() with split_beta=True (tests/test_gpu_dist.py) and equal to
-        the unsplit step() up to fp32 association.  The whitening all-reduce of batch k runs
-        while the experience rows of batch k+1 stream; nothing else waits on the network.
-        Returns the PREVIOUS batch's (loss, stats, dlogits, dvalues) — valid until the next
-        call; with defer_tail, loss / stats are final after wait_stats() — or None on the
-        first call; pipeline_flush() runs the last pending loss.  lp_old / ref_lp and the
-        split buffers are double-buffered."""
+        linearly, so GAE(k+1) needs neither the KL-controller update of loss tail(k) nor
+        anything of L rows(k): it runs as the first workgroups of the L rows(k) launch
+        (trlx_ppo_loss_rows_split_gae), whose rows derive batch k's whitening coefficients
+        from its all-reduced record and apply beta (A = A0 - beta*Ak, rewards, returns).
+        Every loss sees the beta the serial schedule would give it, so losses, stats,
+        gradients and controller state are bit-identical to step() with split_beta=True
+        (tests/test_gpu_dist.py) and equal to the unsplit step() up to fp32 association.  The
+        whitening all-reduce of batch k runs while the experience rows of batch k+1 stream;
+        nothing else waits on the network.  Returns the PREVIOUS batch's (loss, stats,
+        dlogits, dvalues) — valid until the next call; with defer_tail, loss / stats are final
+        after wait_stats() — or None on the first call; pipeline_flush() runs the last pending
+        loss.  lp_old / ref_lp and the split buffers are double-buffered."""
         self._check(logits)
         self._check(ref_logits)
         if logits.stride() != ref_logits.stride():
@@ -649,20 +693,22 @@ class PPOHotPath:
         g_mom, work = self._begin_step(scores, group, s, lag=lag)  # + AR(k) on the side stream (RCCL, no lag)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
         self._experience_rows(logits, ref_logits, labels, s)  # + the deferred loss tail(k-1)
-        self._resolve_allreduce()  # AR(k): GAE(k+1) folds batch k's whitening coefficients
+        self._resolve_allreduce()  # AR(k): the L rows(k) derive batch k's whitening coefficients from it
         if lag:  # batch k's all-reduced score moments (none before the first batch)
             g_mom = self._mom_bufs[prev["buf"]] if prev is not None else None
-        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work, defer_allreduce=True,
-                              fold=self._sbuf[prev["buf"]] if prev is not None else None, lag=lag)
+        # GAE(k+1): its own launch on the first call, else folded into L rows(k)
+        gd = self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work,
+                                   defer_allreduce=True, lag=lag, launch=prev is None or not self._fold_gae)
         out = None
         if prev is not None:
-            self._sidx, self._coef_ready = prev["buf"], True
-            self.adv_stats, self.adv_raw = self._sbuf[prev["buf"]]["stats"], self._sbuf[prev["buf"]]["adv0"]
+            self._use_split(True, prev["buf"])
             self.lp_old, self.ref_lp = self._lp_bufs[prev["buf"]]
             out = self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
-                                   mask=prev["mask"])
-        self._use_split(True, nb)
-        self.lp_old, self.ref_lp = self._lp_bufs[nb]
+                                   mask=prev["mask"], _fold=gd if self._fold_gae else None)
+            self._use_split(True, nb)
+            self.lp_old, self.ref_lp = self._lp_bufs[nb]
+            if self._fold_gae:
+                self._gae_done(gd, s)
         self._pending = dict(buf=nb, new_logits=new_logits, labels=labels, values=values, old_values=old_values,
                              mask=mask)
         return out
