@@ -45,6 +45,14 @@ for st in $steps; do
                 run r03f_ab2_${c}_split_coefl_$i 200 $B --config $c --steps 200 --warmup 5 --schedule serial --split-beta --coef-launch
               done
             done ;;
+        multi) run r03f_host_c2 120 python3 tools/host_overhead.py --config c2
+               run r03f_host_c4 120 python3 tools/host_overhead.py --config c4
+               run r03f_gloo2_c2 300 $B --gpus 2 --backend gloo --steps 40 --warmup 5
+               run r03f_gloo2_c4 300 $B --gpus 2 --backend gloo --config c4 --steps 40 --warmup 5
+               for i in 1 2; do
+                 run r03f_rccl_serial_$i 200 $B --steps 200 --warmup 5 --dist --schedule serial
+                 run r03f_rccl_pipe_$i 200 $B --steps 200 --warmup 5 --dist --schedule pipelined
+               done ;;
         prof) run r03f_prof_c2_pipe 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r03f_prof_c2_pipe -o run -- $B --steps 200 --warmup 5 --schedule pipelined ;;
         *) echo "unknown step $st"; exit 2 ;;
     esac
