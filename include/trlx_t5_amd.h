@@ -64,7 +64,8 @@ const char* trlx_last_error(void);
  * thread's experiment never changes another thread's kernels or summation order.  Keys:
  *   "row_variant"       1 = register-resident vocab rows, 2 = streaming vocab rows
  *   "resident_threads"  workgroup size for resident rows (multiple of 64)
- *   "resident_lb512"    1 = <=512-thread resident rows compiled for 6 waves/SIMD (default 0)
+ *   "resident_lb512"    1 = <=512-thread resident rows compiled for 8 waves/SIMD (default 0; always on
+ *                       for forward rows of <= 8 vectors per thread)
  *   "stream_threads"    workgroup size for streaming rows
  *   "stream_unroll"     16-B loads in flight per thread for streaming rows (2, 4, 8)
  *   "row_order"         resident rows: 0 (default) = step-major vectors, 1 = wave-major

@@ -213,13 +213,16 @@ __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, cons
 // SAME_PHASE: every dlogits row starts at the same address mod 16 as its logits row (the
 // host checks strides and base phases; grad_buffer_like guarantees it), so dlogits are
 // written with the same aligned 16-B vectors.  The other instantiation writes elements.
-// LB512: launched with <= 512 threads, compiled for 6 waves per SIMD (opt-in knob).
+// LB512: launched with <= 512 threads, compiled for 8 waves per SIMD (64 VGPRs): the default
+// for forward rows of <= 8 vectors per thread — T5 / UL2's V = 32128 bf16: four rows in flight
+// per CU instead of three (C4 experience rows 312 -> 306 us, C3 235 -> 232 us; the folded loss
+// tail's blocks spill a few doubles, the row path none) — and an opt-in knob elsewhere.
 // NL > 0 (split residency, long fp32 rows): the row's last NL vector steps are DMA'd into
 // LDS (32 KB per workgroup at NL = 4) instead of VGPRs, so a 512-thread workgroup fits in
 // 128 VGPRs and two rows stay in flight per CU (a 201-KB fp32 row held whole in VGPRs
 // needs 1024 threads at ~88 VGPRs: one row per CU, its load / reduce / store phases exposed).
 template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, int WPE = 4>
-__global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 6 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
+__global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_max2[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
@@ -644,7 +647,7 @@ struct Geometry {
 // Tuning knobs (trlx_set_tuning): 0 = automatic.
 static thread_local int g_row_variant = 0;       // 1 = register-resident rows, 2 = streaming rows
 static thread_local int g_resident_threads = 0;  // preferred workgroup size for resident rows
-static thread_local int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 6 waves/SIMD
+static thread_local int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 8 waves/SIMD
 static thread_local int g_stream_threads = 0;
 static thread_local int g_stream_unroll = 0;
 static thread_local int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
@@ -819,7 +822,7 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     const int rc = rows_grid(a, g.threads, nten, stream, grid, false);
     if (rc) return rc;
     const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
-    const bool lb512 = g.threads <= 512 && g_resident_lb512;
+    const bool lb512 = g.threads <= 512 && (g_resident_lb512 || (MODE == kFwd && g.nv <= 8));
 #define TRLX_RESIDENT_CASE(N)                                                                          \
     case N:                                                                                           \
         if (same && lb512)                                                                            \
