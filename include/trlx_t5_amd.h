@@ -248,7 +248,8 @@ int trlx_ppo_loss_finalize(const double* partials, int64_t nblk, int64_t n,
  *   target-Q rows are only gathered at a* (min over heads) for the expectile V loss (:76-83).
  * Three launches: prep (n_nonterminal = max(1, sum dones[:, :-1]) and sum attention[:, 1:]),
  * rows (one workgroup per vocab row), finalize (fixed-order fp64 sums -> losses[5] =
- * {loss, loss_q, loss_v, loss_cql, loss_awac}).  dvs = d loss / d vs (fp32 [B, A+1], last
+ * {loss, loss_q, loss_v, loss_cql, loss_awac}); prep and finalize run a few workgroups whose
+ * last reduces the block records in fixed order (an arrival ticket in the workspace).  dvs = d loss / d vs (fp32 [B, A+1], last
  * column 0).  Gradient rows have the same strides and 16-B phase as their inputs.  The
  * small [B, .] tensors are contiguous.  No collective: the reference's ILQL loss is
  * rank-local (DDP averages the gradients). */
@@ -277,7 +278,8 @@ typedef struct {
     int64_t dq_sb[2], dq_st[2];
     float* dvs;                       /* [B,A+1] fp32 */
     float* losses;                    /* [5] fp32 */
-    void* workspace;                  /* trlx_ilql_workspace_bytes(B, L, A, nq) bytes */
+    void* workspace;                  /* trlx_ilql_workspace_bytes(B, L, A, nq) bytes, zero-filled
+                                         once before first use (prep / finalize re-arm their tickets) */
 } trlx_ilql_args;
 
 int64_t trlx_ilql_workspace_bytes(int64_t B, int64_t L, int64_t A, int nq);

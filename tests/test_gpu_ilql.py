@@ -240,7 +240,8 @@ def test_ilql_random_sweep(i):
 
 
 @pytest.mark.parametrize("B,L,V,nq,dtype", [(4, 9, 1031, 2, torch.float32), (3, 12, 4097, 1, torch.float32),
-                                            (5, 7, 50257, 2, torch.float32), (4, 10, 2053, 2, torch.bfloat16)])
+                                            (5, 7, 50257, 2, torch.float32), (4, 10, 2053, 2, torch.bfloat16),
+                                            (40, 60, 1031, 2, torch.float32), (70, 33, 257, 1, torch.float32)])
 def test_ilql_hot_path_vs_oracle(B, L, V, nq, dtype):
     """ILQLHotPath.step (the bench's C5 path: prep, rows, finalize into buffers owned by the
     hot path, eager gradients) against the oracle's loss, stats and autograd gradients, over
@@ -265,5 +266,10 @@ def test_ilql_hot_path_vs_oracle(B, L, V, nq, dtype):
         for a, w in zip(dq, wdq):
             torch.testing.assert_close(a.float().cpu(), w, **gr)
         torch.testing.assert_close(dvs.cpu(), wdv.reshape(B, L), rtol=1e-5, atol=1e-6)
+    # prep / finalize: several workgroups at the larger shapes (7120 rows -> 7 finalize
+    # blocks), their arrival tickets re-armed for the next step
+    R = B * L + nq * B * (L - 1)
+    tick = hp.workspace[(16 + 16 * R + 15) // 16 * 16:][:16].view(torch.int32)
+    assert int(tick.abs().sum()) == 0
     with pytest.raises(ValueError):  # head count must match the config
         hp.step(logits.to(DEV), [q.to(DEV) for q in qs[:1]] * (3 - nq), [q.to(DEV) for q in tqs[:1]], vs.to(DEV), bd)

@@ -1,8 +1,9 @@
 // ILQL loss (A10): ILQLConfig.loss of trlx/model/nn/ilql_models.py:52-116 with its autograd,
 // as three launches over the batch (C ABI: trlx_ilql_* in include/trlx_t5_amd.h).
 //
-//   k_ilql_prep      one block: n_nonterminal = max(1, Σ dones[:, :-1]) (:67-68) and
-//                    Σ attention_mask[:, 1:] (:104) -> workspace (fp64)
+//   k_ilql_prep      n_nonterminal = max(1, Σ dones[:, :-1]) (:67-68) and
+//                    Σ attention_mask[:, 1:] (:104) -> workspace (fp64); a few blocks, the
+//                    last to arrive reducing their records in fixed order
 //   k_ilql_rows      one workgroup per vocab row — the logits rows (AWAC cross-entropy,
 //                    :98-105) and the Q-head rows (CQL cross-entropy :87-96 + TD loss
 //                    :63-74); the row is read ONCE into VGPRs (16-B buffer loads, all in
@@ -10,17 +11,28 @@
 //                    gradient g·(onehot − softmax) (+ the TD gradient at the action) is
 //                    written from the same registers.  Thread 0 gathers the target-Q heads
 //                    at the action for the expectile V loss (:76-83) and writes d loss/d vs.
-//   k_ilql_finalize  one block: fixed-order fp64 sums of the per-row records -> the five
-//                    losses of the reference's stats dict (:109-113).
+//   k_ilql_finalize  fixed-order fp64 sums of the per-row records -> the five losses of
+//                    the reference's stats dict (:109-113); blocks over contiguous row
+//                    ranges, the last to arrive reducing their records in fixed order.
+// (Both were single-workgroup launches: 10 + 20 us of one CU's bandwidth per C5 step.)
 // HBM: one read + one write of every logits / Q row (2·V·s bytes per row); target-Q rows
 // cost two scalar gathers.  No MFMA: nothing here is a contraction.
+#include <algorithm>
+
 #include "common.h"
 
 namespace trlx {
 
 constexpr int kIlqlRec = 4;  // floats per row record: {ce·weight, td², v-loss, 0}
+constexpr int kIlqlRedThreads = 256;     // prep / finalize workgroups
+constexpr int kIlqlRedMaxBlocks = 64;
+constexpr int kIlqlPrepPerBlock = 2048;  // dones / attention elements per prep block
+constexpr int kIlqlFinPerBlock = 1024;   // row records per finalize block
 
-// workspace: double[2] {n_nonterminal, Σ attention[:, 1:]} | float[R][kIlqlRec]
+// workspace: double[2] {n_nonterminal, Σ attention[:, 1:]} | float[R][kIlqlRec] | (16-B
+// aligned) uint32 tickets[4] | double prep_rec[64][2] | double fin_rec[64][6].  The tickets
+// must be zero before the first launch (the workspace is zero-filled once; the last block of
+// each reduction re-arms its ticket).
 __host__ __device__ inline int64_t ilql_num_rows(int64_t B, int64_t L, int64_t A, int nq) {
     return B * L + int64_t(nq) * B * A;
 }
@@ -29,6 +41,26 @@ __device__ __forceinline__ const double* ilql_sums(const trlx_ilql_args& a) {
 }
 __device__ __forceinline__ float* ilql_recs(const trlx_ilql_args& a) {
     return reinterpret_cast<float*>(static_cast<char*>(a.workspace) + 16);
+}
+__host__ __device__ inline int64_t ilql_red_offset(int64_t R) {  // tickets, then the block records
+    return (16 + int64_t(sizeof(float)) * kIlqlRec * R + 15) & ~int64_t(15);
+}
+__host__ __device__ inline int ilql_red_blocks(int64_t n, int per) {
+    const int64_t b = (n + per - 1) / per;
+    return int(b < 1 ? 1 : (b > kIlqlRedMaxBlocks ? kIlqlRedMaxBlocks : b));
+}
+struct IlqlRed {
+    unsigned* tickets;
+    double* prep_rec;  // [64][2]
+    double* fin_rec;   // [64][6]
+};
+__device__ __forceinline__ IlqlRed ilql_red(const trlx_ilql_args& a) {
+    char* base = static_cast<char*>(a.workspace) + ilql_red_offset(ilql_num_rows(a.B, a.L, a.A, a.nq));
+    IlqlRed r;
+    r.tickets = reinterpret_cast<unsigned*>(base);
+    r.prep_rec = reinterpret_cast<double*>(base + 16);
+    r.fin_rec = reinterpret_cast<double*>(base + 16 + kIlqlRedMaxBlocks * 2 * sizeof(double));
+    return r;
 }
 
 // Row r of the launch: [0, B·L) logits rows (b, t); then nq blocks of B·A Q-head rows (b, a).
@@ -55,23 +87,34 @@ __device__ __forceinline__ IlqlRowId ilql_decode(const trlx_ilql_args& a, int64_
 }
 
 // ------------------------------------------------------------------ prep
-__global__ __launch_bounds__(kMaxThreads) void k_ilql_prep(trlx_ilql_args a) {
-    __shared__ double sh[(kMaxThreads / kWave) * 2];
+// Block b sums elements [b·chunk, (b+1)·chunk) of dones[:, :-1] and of attention[:, 1:] (same
+// chunk bounds for both index spaces), one fp64 record per block; the last block to arrive
+// reduces the records in block order.
+__global__ __launch_bounds__(kIlqlRedThreads) void k_ilql_prep(trlx_ilql_args a) {
+    __shared__ double sh[(kIlqlRedThreads / kWave) * 2];
     const int64_t S = a.A + 1, L1 = a.L - 1;
+    const int64_t nd = a.B * a.A, na = a.B * L1;
+    const int64_t chunk = (max(nd, na) + gridDim.x - 1) / gridDim.x;
+    const int64_t i0 = int64_t(blockIdx.x) * chunk, i1 = i0 + chunk;
     double st = 0.0, sa = 0.0;
-    for (int64_t i = threadIdx.x; i < a.B * a.A; i += blockDim.x) {
+    for (int64_t i = i0 + threadIdx.x; i < min(i1, nd); i += blockDim.x) {
         const int64_t b = i / a.A;
         st += double(a.dones[b * S + (i - b * a.A)]);
     }
-    for (int64_t i = threadIdx.x; i < a.B * L1; i += blockDim.x) {
+    for (int64_t i = i0 + threadIdx.x; i < min(i1, na); i += blockDim.x) {
         const int64_t b = i / L1;
         sa += double(a.attention_mask[b * a.L + 1 + (i - b * L1)]);
     }
     const double v[2] = {st, sa};
     const double r = block_sum_multi<2>(v, sh);
-    double* out = static_cast<double*>(a.workspace);
-    if (threadIdx.x == 0) out[0] = r > 1.0 ? r : 1.0;  // max(1, terminal_mask.sum())
-    if (threadIdx.x == 1) out[1] = r;
+    const IlqlRed red = ilql_red(a);
+    if (publish_record_last<2>(red.prep_rec + blockIdx.x * 2, r, red.tickets + 0, gridDim.x)) {
+        __syncthreads();  // sh[] reuse
+        const double t = reduce_records<2>(red.prep_rec, int(gridDim.x), sh);
+        double* out = static_cast<double*>(a.workspace);
+        if (threadIdx.x == 0) out[0] = t > 1.0 ? t : 1.0;  // max(1, terminal_mask.sum())
+        if (threadIdx.x == 1) out[1] = t;
+    }
 }
 
 // ------------------------------------------------------------------ rows
@@ -300,15 +343,19 @@ __global__ __launch_bounds__(NL ? 512 : kMaxThreads, NL ? 4 : 1) void k_ilql_row
 }
 
 // ------------------------------------------------------------------ finalize
-__global__ __launch_bounds__(kMaxThreads) void k_ilql_finalize(trlx_ilql_args a) {
-    __shared__ double sh[(kMaxThreads / kWave) * 6];
+// Block b sums the row records [b·chunk, (b+1)·chunk); the last block to arrive reduces the
+// block records in block order and emits the losses.
+__global__ __launch_bounds__(kIlqlRedThreads) void k_ilql_finalize(trlx_ilql_args a) {
+    __shared__ double sh[(kIlqlRedThreads / kWave) * 6];
     __shared__ double tot[6];
     const int64_t nl = a.B * a.L, na = a.B * a.A;
     const int64_t R = ilql_num_rows(a.B, a.L, a.A, a.nq);
+    const int64_t chunk = (R + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = int64_t(blockIdx.x) * chunk, r1 = min(R, r0 + chunk);
     const float* recs = ilql_recs(a);
     // acc: 0 Σ ce·attn (AWAC)  1,2 Σ ce·done per head (CQL)  3,4 Σ td² per head  5 Σ v-loss
     double acc[6] = {0, 0, 0, 0, 0, 0};
-    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) {
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
         const float* rc = recs + r * kIlqlRec;
         if (r < nl) {
             acc[0] += double(rc[0]);
@@ -320,7 +367,11 @@ __global__ __launch_bounds__(kMaxThreads) void k_ilql_finalize(trlx_ilql_args a)
         }
     }
     const double t = block_sum_multi<6>(acc, sh);
-    if (threadIdx.x < 6) tot[threadIdx.x] = t;
+    const IlqlRed red = ilql_red(a);
+    if (!publish_record_last<6>(red.fin_rec + blockIdx.x * 6, t, red.tickets + 1, gridDim.x)) return;
+    __syncthreads();  // sh[] reuse
+    const double f = reduce_records<6>(red.fin_rec, int(gridDim.x), sh);
+    if (threadIdx.x < 6) tot[threadIdx.x] = f;
     __syncthreads();
     if (threadIdx.x == 0) {
         const double* sums = ilql_sums(a);
@@ -424,13 +475,14 @@ static int ilql_launch_rows(const trlx_ilql_args& a, hipStream_t stream) {
 using namespace trlx;
 
 extern "C" int64_t trlx_ilql_workspace_bytes(int64_t B, int64_t L, int64_t A, int nq) {
-    return 16 + int64_t(sizeof(float)) * kIlqlRec * ilql_num_rows(B, L, A, nq);
+    return ilql_red_offset(ilql_num_rows(B, L, A, nq)) + 16 + int64_t(sizeof(double)) * kIlqlRedMaxBlocks * (2 + 6);
 }
 
 extern "C" int trlx_ilql_prep(const trlx_ilql_args* args, void* stream) {
     int rc = ilql_check(args);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_ilql_prep, dim3(1), dim3(kMaxThreads), 0, (hipStream_t)stream, *args);
+    const int nblk = ilql_red_blocks(args->B * std::max(args->A, args->L - 1), kIlqlPrepPerBlock);
+    hipLaunchKernelGGL(k_ilql_prep, dim3(nblk), dim3(kIlqlRedThreads), 0, (hipStream_t)stream, *args);
     return check_launch("k_ilql_prep");
 }
 
@@ -444,7 +496,8 @@ extern "C" int trlx_ilql_rows(const trlx_ilql_args* args, void* stream) {
 extern "C" int trlx_ilql_finalize(const trlx_ilql_args* args, void* stream) {
     int rc = ilql_check(args);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_ilql_finalize, dim3(1), dim3(kMaxThreads), 0, (hipStream_t)stream, *args);
+    const int nblk = ilql_red_blocks(ilql_num_rows(args->B, args->L, args->A, args->nq), kIlqlFinPerBlock);
+    hipLaunchKernelGGL(k_ilql_finalize, dim3(nblk), dim3(kIlqlRedThreads), 0, (hipStream_t)stream, *args);
     return check_launch("k_ilql_finalize");
 }
 

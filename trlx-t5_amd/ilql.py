@@ -91,7 +91,7 @@ class _ILQLLoss(torch.autograd.Function):
         dqs = [grad_buffer_like(q) for q in qs]
         dvs = torch.empty((B, S), dtype=torch.float32, device=dev)
         losses = torch.empty(5, dtype=torch.float32, device=dev)
-        ws = torch.empty(_lib.query("trlx_ilql_workspace_bytes", B, L, A, nq), dtype=torch.uint8, device=dev)
+        ws = torch.zeros(_lib.query("trlx_ilql_workspace_bytes", B, L, A, nq), dtype=torch.uint8, device=dev)
 
         a = _lib.IlqlArgs()
         a.dtype, a.nq, a.B, a.L, a.A, a.V = _lib.dtype_code(lg), nq, B, L, A, V
@@ -197,7 +197,7 @@ class ILQLHotPath:
         self.dvs = torch.empty((B, self.A + 1), dtype=torch.float32, device=self.device)
         self.losses = torch.empty(5, dtype=torch.float32, device=self.device)
         nbytes = _lib.query("trlx_ilql_workspace_bytes", B, L, self.A, self.nq)
-        self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self.workspace = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)  # tickets re-armed in-kernel
         self.dlogits = None
         self.dq = None
         self.timers = None  # optional {name: [[start_event, end_event], ...]}
