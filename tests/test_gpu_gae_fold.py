@@ -15,6 +15,7 @@ import pytest
 import torch
 
 import trlx_t5_amd as P
+from oracle import ppo_oracle as orc
 
 pytestmark = pytest.mark.gpu
 
@@ -303,3 +304,74 @@ def test_two_launch_pipeline_matches_serial(scale):
         for j, (u, v) in enumerate(zip(a, b)):
             assert torch.equal(u, v), f"batch {i} output {j}"
     assert torch.equal(ser_st, pip_st)
+
+
+@pytest.mark.parametrize("i", range(10))
+def test_two_launch_pipeline_fuzz(i):
+    """Seeded random cases of the two-launch pipelined step vs step(split_beta=True): B in
+    [1, 70], T in [1, 140] (one to three GAE scan chunks), V from 2 to 60000 (bf16 / fp32,
+    hosting split kernels, all-VGPR and streaming rows alike), decoder lengths or none, every
+    controller mode or host beta, global or rank-local loss normaliser (no process group),
+    deferred or in-stream loss tails; three batches: every output and the controller record
+    bit-identical."""
+    import random
+    rnd = random.Random(7700 + i)
+    B, Tn = rnd.randint(1, 70), rnd.choice([1, 5, 48, 64, 65, 140])
+    V = [50257, 32128, 2][i] if i < 3 else rnd.randint(2, 60000)
+    B = max(1, min(B, 6_000_000 // (Tn * V)))  # <= 6 M logits per tensor (CPU generation)
+    dt = torch.float32 if i % 3 == 2 else torch.bfloat16
+    lengths = i % 2 == 1 and Tn > 1
+    scale = [None, False, "ref", "running"][i % 4]
+    defer = i % 5 != 0
+    g = torch.Generator().manual_seed(i)
+    batches = []
+    for _ in range(3):
+        logits = torch.randn(B, Tn, V, generator=g).to(dt)
+        Ls = torch.randint(1, Tn + 1, (B,), generator=g) if lengths else None
+        mask = (torch.arange(Tn)[None, :] < Ls[:, None]).long() if lengths else None
+        ov = torch.randn(B, Tn, generator=g)
+        if lengths:
+            ov = ov.masked_fill(mask == 0, 0)
+        batches.append([logits, (logits.float() + 0.1 * torch.randn(B, Tn, V, generator=g)).to(dt),
+                        (logits.float() + 0.05 * torch.randn(B, Tn, V, generator=g)).to(dt),
+                        torch.randint(0, V, (B, Tn), generator=g), ov, ov + 0.3 * torch.randn(B, Tn, generator=g),
+                        torch.rand(B, generator=g) * 24 - 12, Ls, mask])
+    res = {}
+    for mode in ("serial", "pipelined"):
+        cfg = P.PPOConfig(scale_reward=scale if scale is not None else False)
+        ctl = P.PPOControlState.from_config(cfg, DEV, n_steps=B) if scale is not None else None
+        hp = P.PPOHotPath(cfg, B, Tn, V, dt, DEV, kl_coef=0.05, ctl=ctl, defer_tail=defer, split_beta=True)
+        outs = []
+
+        def grab(o):
+            hp.wait_stats()
+            torch.cuda.synchronize()
+            outs.append([t.float().cpu().clone() for t in o] + [hp.rewards.cpu().clone(), hp.returns.cpu().clone()])
+
+        for x in batches:
+            a = [t.to(DEV) for t in x[:7]]
+            kw = dict(lengths=x[7].to(DEV) if x[7] is not None else None, mask=x[8].to(DEV) if x[8] is not None else None)
+            if mode == "pipelined":
+                o = hp.pipeline_step(*a, **kw)
+                if o is not None:
+                    grab(o)
+            else:
+                grab(hp.step(*a, **kw))
+        if mode == "pipelined":
+            grab(hp.pipeline_flush())
+        hp.wait_stats()
+        torch.cuda.synchronize()
+        res[mode] = (outs, ctl.state.cpu().clone() if ctl is not None else None)
+    (ser, ser_st), (pip, pip_st) = res["serial"], res["pipelined"]
+    assert len(ser) == len(pip) == 3
+    for k, (a, b) in enumerate(zip(ser, pip)):
+        for j, (u, v) in enumerate(zip(a, b)):
+            assert torch.equal(u, v), f"case {i} (B {B} T {Tn} V {V} {dt}): batch {k} output {j}"
+    if ser_st is not None:
+        assert torch.equal(ser_st, pip_st)
+    # the serial split step itself vs the oracle on the first batch (fp32 association only)
+    x = batches[0]
+    ref = orc.ppo_step_reference(x[0].float(), x[1].float(), x[2].float(), x[3], x[4], x[5], x[6],
+                                 kl_coef=0.05, lengths=x[7], mask=x[8]) if scale is None else None
+    if ref is not None:
+        torch.testing.assert_close(ser[0][0].reshape(()), ref["loss"], rtol=1e-4, atol=1e-5)
