@@ -25,12 +25,12 @@ namespace trlx {
 
 constexpr int kIlqlRec = 4;  // floats per row record: {ce·weight, td², v-loss, 0}
 constexpr int kIlqlRedThreads = 256;     // prep / finalize workgroups
-constexpr int kIlqlRedMaxBlocks = 64;
-constexpr int kIlqlPrepPerBlock = 2048;  // dones / attention elements per prep block
-constexpr int kIlqlFinPerBlock = 1024;   // row records per finalize block
+constexpr int kIlqlRedMaxBlocks = 128;
+constexpr int kIlqlPrepPerBlock = 256;   // dones / attention elements per prep block (C5: 10.8 -> 5.4 us vs 2048)
+constexpr int kIlqlFinPerBlock = 1024;   // row records per finalize block (256 / 512: 17 / 14 us vs 12)
 
 // workspace: double[2] {n_nonterminal, Σ attention[:, 1:]} | float[R][kIlqlRec] | (16-B
-// aligned) uint32 tickets[4] | double prep_rec[64][2] | double fin_rec[64][6].  The tickets
+// aligned) uint32 tickets[4] | double prep_rec[128][2] | double fin_rec[128][6].  The tickets
 // must be zero before the first launch (the workspace is zero-filled once; the last block of
 // each reduction re-arms its ticket).
 __host__ __device__ inline int64_t ilql_num_rows(int64_t B, int64_t L, int64_t A, int nq) {
@@ -51,8 +51,8 @@ __host__ __device__ inline int ilql_red_blocks(int64_t n, int per) {
 }
 struct IlqlRed {
     unsigned* tickets;
-    double* prep_rec;  // [64][2]
-    double* fin_rec;   // [64][6]
+    double* prep_rec;  // [kIlqlRedMaxBlocks][2]
+    double* fin_rec;   // [kIlqlRedMaxBlocks][6]
 };
 __device__ __forceinline__ IlqlRed ilql_red(const trlx_ilql_args& a) {
     char* base = static_cast<char*>(a.workspace) + ilql_red_offset(ilql_num_rows(a.B, a.L, a.A, a.nq));
@@ -355,15 +355,17 @@ __global__ __launch_bounds__(kIlqlRedThreads) void k_ilql_finalize(trlx_ilql_arg
     const float* recs = ilql_recs(a);
     // acc: 0 Σ ce·attn (AWAC)  1,2 Σ ce·done per head (CQL)  3,4 Σ td² per head  5 Σ v-loss
     double acc[6] = {0, 0, 0, 0, 0, 0};
+    static_assert(kIlqlRec == 4, "one 16-B load per record");
     for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-        const float* rc = recs + r * kIlqlRec;
+        const vec4u rv = *reinterpret_cast<const vec4u*>(recs + r * kIlqlRec);
+        const float c0 = __uint_as_float(rv.x), c1 = __uint_as_float(rv.y), c2 = __uint_as_float(rv.z);
         if (r < nl) {
-            acc[0] += double(rc[0]);
+            acc[0] += double(c0);
         } else {
             const int h = int((r - nl) / na);
-            acc[1 + h] += double(rc[0]);
-            acc[3 + h] += double(rc[1]);
-            acc[5] += double(rc[2]);
+            acc[1 + h] += double(c0);
+            acc[3 + h] += double(c1);
+            acc[5] += double(c2);
         }
     }
     const double t = block_sum_multi<6>(acc, sh);
