@@ -67,6 +67,15 @@ def test_fresh_build_exports_exactly_the_header(fresh_lib):
     assert set(re.findall(r"\bT (trlx_\w+)", in_tree)) == exported, "in-tree .so is stale: rebuild with make"
 
 
+def test_capi_consumer_builds_against_the_fresh_library(fresh_lib, tmp_path):
+    """tests/capi/capi_check.cpp (a C++ caller of the C ABI, no torch) compiles and links
+    against the library built from HEAD's sources."""
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "capi"), f"OUT={tmp_path / 'capi_check'}",
+                        f"LIBDIR={os.path.dirname(fresh_lib)}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert os.path.exists(tmp_path / "capi_check")
+
+
 def test_library_is_gfx950_code(built_lib):
     assert b"gfx950" in open(_lib.LIB_PATH, "rb").read()
 
