@@ -53,6 +53,11 @@ for st in $steps; do
                  run r03f_rccl_serial_$i 200 $B --steps 200 --warmup 5 --dist --schedule serial
                  run r03f_rccl_pipe_$i 200 $B --steps 200 --warmup 5 --dist --schedule pipelined
                done ;;
+        strong) for i in 1 2; do
+                  run r03f_strong_serial_$i 200 $B --config c4 --global-batch 1024 --steps 50 --warmup 5 --schedule serial
+                  run r03f_strong_split_$i 200 $B --config c4 --global-batch 1024 --steps 50 --warmup 5 --schedule serial --split-beta
+                  run r03f_strong_pipe_$i 200 $B --config c4 --global-batch 1024 --steps 50 --warmup 5 --schedule pipelined
+                done ;;
         prof) run r03f_prof_c2_pipe 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r03f_prof_c2_pipe -o run -- $B --steps 200 --warmup 5 --schedule pipelined ;;
         *) echo "unknown step $st"; exit 2 ;;
     esac
