@@ -175,19 +175,23 @@ def dry_run(args):
             raise SystemExit(3)
 
 
-def algorithmic_bytes(V, s, masked, pipelined=False):
+def algorithmic_bytes(V, s, masked, pipelined=False, fill=1.0):
     """Minimum HBM bytes per response token, per launch.  Each [B,T] fp32
     vector read or written once counts 4 B; int64 labels / mask 8 B.  pipelined: the
     split-beta kernels (GAE -> A0, Ak, kl, score terms; the loss rows finish rewards and
-    returns), the GAE riding the loss rows launch."""
+    returns), the GAE riding the loss rows launch.  fill (a ragged batch, C3): the fraction
+    of decoder positions inside their rollout's length — only those logits rows are read
+    (experience: store padding past the length; loss: mask == 0), while every dlogits row is
+    written (zeros where masked)."""
     mask_b = 8 if masked else 0
-    exp = 2 * V * s + 8 + 2 * 4                     # K1 rows: policy + ref row, label -> lp, ref_lp
+    exp = 2 * V * s * fill + 8 + 2 * 4             # K1 rows: policy + ref row, label -> lp, ref_lp
+    row = V * s * fill + V * s                      # loss row read + dlogits row written
     if pipelined:
         gae = 3 * 4 + 4 * 4 + mask_b               # lp, ref_lp, values -> adv0, adv_kl, rew_kl, rew_score
-        loss = 2 * V * s + 8 + 4 * 7 + 4 * 4 + mask_b + gae  # row + dlogits, label, 7 vectors -> lp, dv, rewards, returns
+        loss = row + 8 + 4 * 7 + 4 * 4 + mask_b + gae  # row + dlogits, label, 7 vectors -> lp, dv, rewards, returns
     else:
         gae = 2 * 4 + 4 + 3 * 4 + mask_b           # lp, ref_lp, values -> rewards, adv, returns
-        loss = 2 * V * s + 8 + 4 * 6 + 2 * 4 + mask_b  # K2 rows: row + dlogits, label, 6 vectors -> lp, dv
+        loss = row + 8 + 4 * 6 + 2 * 4 + mask_b    # K2 rows: row + dlogits, label, 6 vectors -> lp, dv
     lred = 11 * 4                                  # per-token loss record read back
     return {"experience": exp, "loss": loss, "step": exp + gae + loss + lred - (gae if pipelined else 0)}
 
@@ -522,7 +526,9 @@ def main():
         schedule = "pipelined" if args.schedule in ("pipelined", "auto") else "serial"
         names = {"experience", "loss"}
         tokens = B * T
-        ab = algorithmic_bytes(V, 4 if args.logits_dtype == "fp32" else 2, masked, schedule == "pipelined")
+        # ragged batch (C3): the share of positions inside their rollout's decoder length
+        fill = float(x["lengths"].sum().item()) / tokens if masked else 1.0
+        ab = algorithmic_bytes(V, 4 if args.logits_dtype == "fp32" else 2, masked, schedule == "pipelined", fill)
         doms = ("experience", "loss")
         # PMC bytes were collected at the config's rows per GPU
         traffic_key = None if args.global_batch else args.config + ("_fp32" if args.logits_dtype == "fp32" else "")
@@ -581,6 +587,11 @@ def main():
             "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world, "seq_len": T, "vocab": V,
                        "logits_dtype": "fp32" if ilql else args.logits_dtype, "tokens_per_gpu_step": tokens,
                        "parallelism": f"dp{world}", "schedule": schedule, "comm": comm_kind},
+            **({"ragged": {"valid_token_fraction": round(fill, 4),
+                           "note": "tokens counts every decoder position of the padded batch; logits rows past a "
+                                   "rollout's length are store padding (lp = 0) and masked loss rows have zero "
+                                   "gradient, so neither is read (roofline bytes count only the rows read)"}}
+               if masked and not ilql else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRLX_ABI_VERSION 1
+#define TRLX_ABI_VERSION 2
 
 typedef enum {
     TRLX_F32 = 0,
@@ -91,6 +91,14 @@ int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype,
                         const int64_t* labels, int64_t lb, int64_t lt,
                         void* out_lp0, void* out_lp1, int out_dtype,
                         float* out_lse0, float* out_lse1, void* stream);
+/* The experience rows of a ragged batch (decoder lengths [B] int64): a row (b, t) with
+ * t >= lengths[b] is store padding — ppo_pipeline.py:47-65 pads each element's logprobs with
+ * 0.0 — so its lp is 0 and the row is NOT read (the bytes of a batch of decoder lengths L_b
+ * are those of its sum(L_b) tokens).  lengths == NULL: trlx_lsm_gather_fwd. */
+int trlx_lsm_gather_fwd_ragged(const void* x0, const void* x1, int dtype,
+                               int64_t B, int64_t T, int64_t V, int64_t sb, int64_t st,
+                               const int64_t* labels, int64_t lb, int64_t lt, const int64_t* lengths,
+                               void* out_lp0, void* out_lp1, int out_dtype, void* stream);
 
 /* ---------------------------------------------------------------- A1 backward
  * Autograd of modeling.py:39-40 (log_softmax_backward of the gathered one-hot):
@@ -158,7 +166,9 @@ int trlx_whiten_apply(const void* x, int dtype, int64_t n, const double* stats, 
  * once.  Advantages are whitened on the fly from adv_raw + stats (stats == NULL: adv is
  * used as given).  mask: int64 [B,T] or NULL (all ones); msum: device fp64 scalar (NULL:
  * use msum_host).  Outputs: lp_out fp32 [B,T]; dx (row (b,t) at dx + b*dsb + t*dst, dtype
- * of x). */
+ * of x).  A masked token (mask == 0) has d loss / d lp = 0 exactly, so its dlogits row is
+ * written as zeros WITHOUT reading its logits and lp_out is 0 there (for every loss-rows
+ * entry point below as well; the token's loss terms are those of any finite lp). */
 int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_t T, int64_t V,
                           int64_t sb, int64_t st, const int64_t* labels, int64_t lb, int64_t lt,
                           const void* old_lp, int old_dtype, const float* adv,
@@ -178,7 +188,10 @@ int trlx_ppo_policy_fused(const void* x, int dtype, int64_t B, int64_t T, int64_
  * all-reduced across ranks in between) whitens the advantages on the fly; unbiased as in
  * trlx_whiten_apply.  workspace: trlx_ppo_workspace_bytes(B, T) bytes, zero-filled once
  * before the first use and then reusable (the kernels re-arm their tickets).  Rows (b, t)
- * of the rollout batch must be contiguous rollouts (t fastest). */
+ * of the rollout batch must be contiguous rollouts (t fastest).  With lengths, the
+ * experience rows past each rollout's length are store padding (lp = ref_lp = 0, not read:
+ * trlx_lsm_gather_fwd_ragged); with a mask, the loss rows of masked tokens are not read
+ * (trlx_ppo_policy_fused). */
 int64_t trlx_ppo_workspace_bytes(int64_t B, int64_t T);
 int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dtype, int64_t B, int64_t T,
                               int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
@@ -187,7 +200,7 @@ int trlx_ppo_experience_fused(const void* logits, const void* ref_logits, int dt
                               float lam, float* lp, float* ref_lp, float* rewards, float* adv_raw,
                               void* ret, int ret_dtype, double* stats, void* workspace, void* stream);
 /* The two launches of each fused entry point, separately (same arguments):
- *   experience = trlx_lsm_gather_fwd(policy, ref -> fp32 lp, ref_lp) + trlx_ppo_rollout_gae
+ *   experience = trlx_lsm_gather_fwd_ragged(policy, ref -> fp32 lp, ref_lp) + trlx_ppo_rollout_gae
  *   loss       = trlx_ppo_loss_rows + trlx_ppo_rollout_loss  */
 int trlx_ppo_rollout_gae(int64_t B, int64_t T, const float* lp, const float* ref_lp, const void* values,
                          int v_dtype, const float* scores, const int64_t* lengths, const int64_t* mask,
@@ -431,10 +444,12 @@ int trlx_ppo_rollout_loss_ctl(int64_t B, int64_t T, const double* stats, float v
  * reduction and its launch leave the critical path and no cross-stream event is needed.
  * Kernels that cannot host it (the streaming rows) run the tail as its own launch first.
  * Stream order is that of the two calls: the tail reads the token records of the loss rows
- * launched before, the GAE tail launched after reads the KL coefficient it updates. */
+ * launched before, the GAE tail launched after reads the KL coefficient it updates.
+ * lengths: as in trlx_lsm_gather_fwd_ragged (NULL: every row). */
 int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int64_t B, int64_t T, int64_t V,
                                   int64_t sb, int64_t st, const int64_t* labels, int64_t lb, int64_t lt,
-                                  void* out_lp0, void* out_lp1, int out_dtype, int64_t tail_B, int64_t tail_T,
+                                  const int64_t* lengths, void* out_lp0, void* out_lp1, int out_dtype,
+                                  int64_t tail_B, int64_t tail_T,
                                   const double* tail_stats, float vf_coef, float* loss, float* loss_stats,
                                   void* workspace, const trlx_kl_ctl* kl, void* stream);
 

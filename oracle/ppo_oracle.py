@@ -183,6 +183,14 @@ class ScoreControl:
         return scores, batch_mean, batch_std
 
 
+def store_padded(x, lengths):
+    """A per-token [B, T] tensor as the padded store returns it (ppo_pipeline.py:47-65): each
+    element covers its own decoder length and the collate pads with 0.0 (lengths None: as is)."""
+    if lengths is None:
+        return x
+    return x.masked_fill(torch.arange(x.shape[1])[None, :] >= lengths[:, None], 0)
+
+
 def kl_penalty_rewards(logprobs, ref_logprobs, kl_coef, scores=None, lengths=None):
     """ppo_orchestrator.py:164-167.  With `lengths` (build extension for the padded store,
     ppo_pipeline.py:47-65): the score goes to column lengths[b]-1 and later columns are 0."""
@@ -207,17 +215,21 @@ def ppo_step_reference(logits, ref_logits, new_logits, labels, old_values, value
     """The bench step with the reference's own ops: experience (ppo_orchestrator.py:154-167)
     then the loss side of accelerate_ppo_model.py:88-126 with autograd backward.  Runs in
     the inputs' dtype (fp32 on bf16-quantised inputs = the parity oracle; native bf16 = the
-    reference T5/UL2 path, the timed CPU baseline).  old_lp for the loss = experience lp."""
+    reference T5/UL2 path, the timed CPU baseline).  old_lp for the loss = experience lp.
+    new_lp is returned at every position; the build's loss rows write 0 where mask == 0
+    (nothing depends on it there, so those rows are not read)."""
     cfg = dict(gamma=1, lam=0.95, cliprange=0.2, cliprange_value=0.2, vf_coef=1)
     cfg.update(cfg_kwargs or {})
     B, T = labels.shape
     with torch.no_grad():
         lp = logprobs_from_logits(logits, labels)
         ref_lp = logprobs_from_logits(ref_logits, labels)
-        rewards = kl_penalty_rewards(lp, ref_lp, kl_coef, scores, lengths)
         ov = old_values
         if lengths is not None:
-            ov = old_values.masked_fill(torch.arange(T)[None, :] >= lengths[:, None], 0)
+            # a ragged batch: the padded store's tensors (ppo_pipeline.py:47-65) — each element's
+            # logprobs / values cover its own decoder length, the collate pads them with 0.0
+            lp, ref_lp, ov = store_padded(lp, lengths), store_padded(ref_lp, lengths), store_padded(ov, lengths)
+        rewards = kl_penalty_rewards(lp, ref_lp, kl_coef, scores, lengths)
     if mask is None:
         mask = torch.ones((B, T), dtype=torch.long)
     adv, ret = gae(ov, rewards, T, cfg["gamma"], cfg["lam"], use_whitening=True)

@@ -13,3 +13,9 @@ def T(arr, bf16=None):
 
 def is_bf16(arr):
     return np.asarray(arr).dtype == np.uint16
+
+
+def loss_rows_lp(new_lp, mask):
+    """The loss rows' lp_out: the logprob where mask != 0 and 0 at masked tokens (their rows
+    are not read: d loss / d lp is 0 there and no output depends on lp)."""
+    return new_lp if mask is None else new_lp.masked_fill(mask == 0, 0)

@@ -56,8 +56,8 @@ def test_dp2_step_global_whitening(lengths, mode):
 
     # oracle: experience per row, GAE per row, whitening with the GLOBAL biased moments
     f = {k: (v.float() if v is not None and v.is_floating_point() else v) for k, v in x.items()}
-    lp = orc.logprobs_from_logits(f["logits"], x["labels"])
-    ref_lp = orc.logprobs_from_logits(f["ref_logits"], x["labels"])
+    lp = orc.store_padded(orc.logprobs_from_logits(f["logits"], x["labels"]), x["lengths"])
+    ref_lp = orc.store_padded(orc.logprobs_from_logits(f["ref_logits"], x["labels"]), x["lengths"])
     rewards = orc.kl_penalty_rewards(lp, ref_lp, 0.05, x["scores"], x["lengths"])
     adv, ret = orc.gae(x["old_values"], rewards, T, 1.0, 0.95, use_whitening=False)
     mu = adv.double().mean()
@@ -159,8 +159,8 @@ def test_dp2_step_global_loss_norm():
         assert p.exitcode == 0
 
     f = {k: (v.float() if v is not None and v.is_floating_point() else v) for k, v in x.items()}
-    lp = orc.logprobs_from_logits(f["logits"], x["labels"])
-    ref_lp = orc.logprobs_from_logits(f["ref_logits"], x["labels"])
+    lp = orc.store_padded(orc.logprobs_from_logits(f["logits"], x["labels"]), x["lengths"])
+    ref_lp = orc.store_padded(orc.logprobs_from_logits(f["ref_logits"], x["labels"]), x["lengths"])
     rewards = orc.kl_penalty_rewards(lp, ref_lp, 0.05, x["scores"], x["lengths"])
     adv, ret = orc.gae(x["old_values"], rewards, T, 1.0, 0.95, use_whitening=False)
     mu = adv.double().mean()

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TRLX_T5_AMD_LIB") or os.path.join(_HERE, "libtrlx_t5_amd.so")
 
 F32, BF16, I64 = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
 MOMENT_SLOTS = 4
 SPLIT_MOMENT_SLOTS = 8  # split-beta record {Σ A0, Σ A0², n, Σ Ak, Σ A0·Ak, Σ Ak², Σ mask, 0}
 PPO_STATS = 13
@@ -82,6 +82,8 @@ SIGNATURES = {
     "trlx_set_tuning": (_c_int, [ctypes.c_char_p, _c_i64]),
     "trlx_lsm_gather_fwd": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                      _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
+    "trlx_lsm_gather_fwd_ragged": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
+                                            _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
     "trlx_lsm_gather_bwd": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
                                      _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_i64, _c_i64, _c_vp]),
     "trlx_kl_penalty_rewards": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_f, _c_vp, _c_vp,
@@ -159,8 +161,8 @@ SIGNATURES = {
     "trlx_comm_allreduce_sum_f64": (_c_int, [_c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_comm_destroy": (_c_int, [_c_vp]),
     "trlx_lsm_gather_fwd_loss_tail": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
-                                               _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_vp, _c_f,
-                                               _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
+                                               _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_vp,
+                                               _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
     "trlx_ilql_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_int]),
     "trlx_ilql_prep": (_c_int, [_ilql_p, _c_vp]),
     "trlx_ilql_rows": (_c_int, [_ilql_p, _c_vp]),

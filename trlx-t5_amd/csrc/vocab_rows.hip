@@ -80,6 +80,8 @@ struct RowArgs {
     const double* wctl;
     float wbeta;
     float* coef_out;
+    // forward rows of a ragged batch: rows (b, t >= lengths[b]) are store padding (pad_row)
+    const int64_t* lengths;
 };
 
 // ------------------------------------------------------------------ shared row pieces
@@ -209,6 +211,53 @@ __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, cons
         loss_token_terms(a.ltok, a.tokrec, row, pt, ps.m, ps.inv_msum, vin[0], vin[1], vin[2]);
 }
 
+// ------------------------------------------------------------------ rows that are not read
+// Ragged batches.  A decoder position past its rollout's length (forward rows, `lengths`
+// given) is store padding: the reference's collate pads each element's logprobs with 0.0
+// (ppo_pipeline.py:47-65) and the GAE reads nothing past the length, so lp = 0 there and the
+// row is not read.  A masked token of the loss (mask == 0) has dloss/dlp = 0 exactly (every
+// path from lp to the loss is multiplied by the mask, ppo_models.py:165-177), so its dlogits
+// row g·(onehot − p) is zeros, and lp reaches no other output: log_ratio = (lp − olp)·0 = 0
+// for every finite lp, which the token record below uses with lp = 0 (lp_out = 0).  The
+// row is written as zeros without being read.  (A masked row of non-finite logits made the
+// reference's loss NaN through NaN·0; here it is not read at all — DESIGN.md §7.)  Both
+// checks are block-uniform scalar loads ahead of the row; without lengths / mask the
+// launches skip them.
+__device__ __forceinline__ bool pad_row(const RowArgs& a) {
+    const int64_t row = int64_t(blockIdx.x) - a.lead_blocks;
+    const int64_t b = row / a.T;
+    if (row - b * a.T < a.lengths[b]) return false;
+    if (threadIdx.x == 0) {
+        st_any(blockIdx.y == 0 ? a.lp0 : a.lp1, a.out_dtype, row, 0.0f);
+        float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
+        if (lse_out) lse_out[row] = 0.0f;
+    }
+    return true;
+}
+
+template <class DT>
+__device__ __forceinline__ void masked_row(const RowArgs& a, int64_t row) {
+    typedef typename DT::elem_t E;
+    const int64_t b = row / a.T, t = row - b * a.T;
+    E* drow = reinterpret_cast<E*>(a.dx) + b * a.dsb + t * a.dst;
+    const RowSplit<DT> s(drow, a.V);  // the gradient row's own 16-B phase
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(drow + s.head, uint32_t(s.nvec) * 16u);
+    const vec4u z = {0u, 0u, 0u, 0u};
+    for (int i = tid; i < int(s.nvec); i += nthr) store_grad_b128(z, rout, i * 16, a.spol);
+    if (tid < s.head) DT::store1(drow, tid, 0.0f);
+    if (tid < s.tail) DT::store1(drow, s.tail0 + tid, 0.0f);
+    if (tid == 0) {
+        float vin[3];
+        const PpoScalars p = ppo_scalars(a, row, vin, true);
+        PolicyTerms pt;
+        ppo_policy_dlp(0.0f, p.olp, p.A, p.m, p.inv_msum, a.cliprange, pt);
+        a.lp_out[row] = 0.0f;
+        token_record(a, row, pt, p, vin);
+        if (a.coef || a.wstats) split_outputs(a, row, p);
+    }
+}
+
 // ------------------------------------------------------------------ register-resident rows
 // SAME_PHASE: every dlogits row starts at the same address mod 16 as its logits row (the
 // host checks strides and base phases; grad_buffer_like guarantees it), so dlogits are
@@ -239,6 +288,18 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL 
             __shared__ double gae_red[kMaxThreads / kWave * 8];
             gae_block<true>(a.gae, int(blockIdx.x), a.gae_blocks, gae_red);
             return;
+        }
+    }
+    if constexpr (MODE == kFwd) {
+        if (a.lengths && pad_row(a)) return;
+    }
+    if constexpr (MODE == kPpo) {
+        if (a.mask) {
+            const int64_t row = int64_t(blockIdx.x) - a.lead_blocks;
+            if (a.mask[row] == 0) {
+                masked_row<DT>(a, row);
+                return;
+            }
         }
     }
     typedef typename DT::elem_t E;
@@ -513,6 +574,15 @@ template <class DT, int U, int MODE>
 __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs a) {
     __shared__ float sh_m[kStreamMaxThreads / kWave];
     __shared__ float sh_s[kStreamMaxThreads / kWave];
+    if constexpr (MODE == kFwd) {
+        if (a.lengths && pad_row(a)) return;
+    }
+    if constexpr (MODE == kPpo) {
+        if (a.mask && a.mask[blockIdx.x] == 0) {
+            masked_row<DT>(a, int64_t(blockIdx.x));
+            return;
+        }
+    }
     typedef typename DT::elem_t E;
     constexpr int EPV = DT::kEPV;
     const int tid = threadIdx.x, nthr = blockDim.x;
@@ -898,18 +968,34 @@ extern "C" int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype, in
     return launch_rows<kFwd>(a, dtype, x1 ? 2 : 1, (hipStream_t)stream);
 }
 
+extern "C" int trlx_lsm_gather_fwd_ragged(const void* x0, const void* x1, int dtype, int64_t B, int64_t T,
+                                          int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
+                                          int64_t lt, const int64_t* lengths, void* out_lp0, void* out_lp1,
+                                          int out_dtype, void* stream) {
+    RowArgs a = {};
+    a.x0 = x0; a.x1 = x1; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
+    a.labels = labels; a.lb = lb; a.lt = lt; a.lengths = lengths;
+    a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype;
+    if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;
+    int rc = check_rows(a, dtype);
+    if (rc) return rc;
+    TRLX_REQUIRE(out_lp0 && (!x1 || out_lp1), TRLX_ERR_ARG, "NULL logprob output");
+    TRLX_REQUIRE(out_dtype == TRLX_F32 || out_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "out dtype");
+    return launch_rows<kFwd>(a, dtype, x1 ? 2 : 1, (hipStream_t)stream);
+}
+
 static int fill_loss_tail(LossRolloutArgs* L, int64_t B, int64_t T, const double* stats, float vf_coef, float* loss,
                           float* loss_stats, void* workspace, const trlx_kl_ctl* kl);
 
 extern "C" int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int64_t B, int64_t T,
                                              int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
-                                             int64_t lt, void* out_lp0, void* out_lp1, int out_dtype, int64_t tail_B,
-                                             int64_t tail_T, const double* tail_stats, float vf_coef, float* loss,
-                                             float* loss_stats, void* workspace, const trlx_kl_ctl* kl,
-                                             void* stream) {
+                                             int64_t lt, const int64_t* lengths, void* out_lp0, void* out_lp1,
+                                             int out_dtype, int64_t tail_B, int64_t tail_T, const double* tail_stats,
+                                             float vf_coef, float* loss, float* loss_stats, void* workspace,
+                                             const trlx_kl_ctl* kl, void* stream) {
     RowArgs a = {};
     a.x0 = x0; a.x1 = x1; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
-    a.labels = labels; a.lb = lb; a.lt = lt;
+    a.labels = labels; a.lb = lb; a.lt = lt; a.lengths = lengths;
     a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype;
     int rc = fill_loss_tail(&a.tail, tail_B, tail_T, tail_stats, vf_coef, loss, loss_stats, workspace, kl);
     if (rc) return rc;
@@ -1075,8 +1161,8 @@ extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_log
                                          float* rewards, float* adv_raw, void* ret, int ret_dtype,
                                          double* stats, void* workspace, void* stream) {
     TRLX_REQUIRE(ref_logits, TRLX_ERR_ARG, "NULL reference logits");
-    int rc = trlx_lsm_gather_fwd(logits, ref_logits, dtype, B, T, V, sb, st, labels, lb, lt, lp, ref_lp, TRLX_F32,
-                                 nullptr, nullptr, stream);
+    int rc = trlx_lsm_gather_fwd_ragged(logits, ref_logits, dtype, B, T, V, sb, st, labels, lb, lt, lengths, lp,
+                                        ref_lp, TRLX_F32, stream);
     if (rc) return rc;
     return trlx_ppo_rollout_gae(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, gamma, lam,
                                 rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);

@@ -297,7 +297,7 @@ class PPOHotPath:
         s = torch.cuda.current_stream(self.device)
         self._use_split(self.split_beta, 0)
         g_mom, work = self._begin_step(scores, group, s)
-        self._experience_rows(logits, ref_logits, labels, s)
+        self._experience_rows(logits, ref_logits, labels, s, lengths)
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
         return self.lp_old, self.ref_lp
 
@@ -317,19 +317,24 @@ class PPOHotPath:
         else:
             self.adv_stats, self.adv_raw = self._stats4, self._adv_raw4
 
-    def _experience_rows(self, logits, ref_logits, labels, s, b0=0, timed=True):
-        """Policy + reference rows of rollouts [b0, b0 + logits.shape[0]) -> lp_old, ref_lp."""
+    def _experience_rows(self, logits, ref_logits, labels, s, lengths=None, b0=0, timed=True):
+        """Policy + reference rows of rollouts [b0, b0 + logits.shape[0]) -> lp_old, ref_lp.
+        lengths (a ragged batch): rows past each rollout's length are store padding, lp = 0,
+        not read (trlx_lsm_gather_fwd_ragged)."""
         B, T, V = logits.shape[0], self.T, self.V
         rows = (logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V, logits.stride(0),
-                logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1), self.lp_old[b0].data_ptr(),
-                self.ref_lp[b0].data_ptr(), _lib.F32)
+                logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1))
+        outs = (self.lp_old[b0].data_ptr(), self.ref_lp[b0].data_ptr(), _lib.F32)
         if timed:
             self._ev("experience", s)
         if self._tail_pending is not None:  # the previous step's loss tail rides this launch
             pend, self._tail_pending = self._tail_pending, None
-            _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, *self._tail_args(pend), s.cuda_stream)
+            _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, _lib.ptr(lengths), *outs, *self._tail_args(pend),
+                      s.cuda_stream)
+        elif lengths is not None:
+            _lib.call("trlx_lsm_gather_fwd_ragged", *rows, lengths.data_ptr(), *outs, s.cuda_stream)
         else:
-            _lib.call("trlx_lsm_gather_fwd", *rows, None, None, s.cuda_stream)
+            _lib.call("trlx_lsm_gather_fwd", *rows, *outs, None, None, s.cuda_stream)
         if timed:
             self._ev_end("experience", s)
 
@@ -408,7 +413,8 @@ class PPOHotPath:
                 x0, x1 = self.lm_logits[0, :nb], self.lm_logits[1, :nb]
                 torch.matmul(hidden[b0:b0 + nb], weight.t(), out=x0)
                 torch.matmul(ref_hidden[b0:b0 + nb], ref_weight.t(), out=x1)
-                self._experience_rows(x0, x1, labels[b0:b0 + nb], s, b0=b0, timed=False)
+                self._experience_rows(x0, x1, labels[b0:b0 + nb], s, None if lengths is None else lengths[b0:b0 + nb],
+                                      b0=b0, timed=False)
             self._ev_end("experience", s)
             self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
             return self.lp_old, self.ref_lp
@@ -692,7 +698,7 @@ class PPOHotPath:
         self._lag = lag
         g_mom, work = self._begin_step(scores, group, s, lag=lag)  # + AR(k) on the side stream (RCCL, no lag)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
-        self._experience_rows(logits, ref_logits, labels, s)  # + the deferred loss tail(k-1)
+        self._experience_rows(logits, ref_logits, labels, s, lengths)  # + the deferred loss tail(k-1)
         self._resolve_allreduce()  # AR(k): the L rows(k) derive batch k's whitening coefficients from it
         if lag:  # batch k's all-reduced score moments (none before the first batch)
             g_mom = self._mom_bufs[prev["buf"]] if prev is not None else None
