@@ -203,3 +203,4 @@ def test_ragged_pipeline_matches_step():
         for a, b in zip(w, g):
             assert torch.equal(a, b)
         assert bool(torch.isfinite(g[0]).all()) and bool(torch.isfinite(g[2].float()).all())
+

@@ -40,21 +40,21 @@ def main():
             "random": (L, (ar < L[:, None]).long())}
     Ls = torch.sort(L, descending=True).values
     pats["sorted"] = (Ls, (ar < Ls[:, None]).long())
-    res = {k: [] for k in pats}
+    res = {n: [] for n in pats}
     for rnd in range(a.rounds):
-        for name, (lens, mask) in pats.items():
-            x["lengths"], x["mask"] = lens, mask
+        for key in pats:
+            x["lengths"], x["mask"] = pats[key]
             bench.settle_and_warm(step, torch, ns, dev)
             el, km, _ = bench.timed_run(step, hp, torch, dist, ns, dev, 1, {"experience", "loss"})
-            res[name].append((el / a.steps * 1e3, km["experience"] * 1e3, km["loss"] * 1e3))
-            print(f"round {rnd} {name:7s} step {res[name][-1][0]:.4f} ms  E {res[name][-1][1]:7.2f} us  "
-                  f"L {res[name][-1][2]:7.2f} us", flush=True)
+            res[key].append((el / a.steps * 1e3, km["experience"] * 1e3, km["loss"] * 1e3))
+            print(f"round {rnd} {key:12s} step {res[key][-1][0]:.4f} ms  E {res[key][-1][1]:7.2f} us  "
+                  f"L {res[key][-1][2]:7.2f} us", flush=True)
     fill = float(L.sum()) / (B * T)
     print(f"{a.config} {B}x{T}x{V}: random fill {fill:.4f}")
     for name, r in res.items():
         r = sorted(r)
         m = r[len(r) // 2]
-        print(f"median {name:7s} step {m[0]:.4f} ms  E {m[1]:7.2f} us  L {m[2]:7.2f} us")
+        print(f"median {name:12s} step {m[0]:.4f} ms  E {m[1]:7.2f} us  L {m[2]:7.2f} us")
 
 
 if __name__ == "__main__":

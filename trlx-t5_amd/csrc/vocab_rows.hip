@@ -93,8 +93,9 @@ struct Row {
     int64_t y;
     bool y_ok;
     RowSplit<DT> s;
-    __device__ __forceinline__ Row(const RowArgs& a)
-        : row(int64_t(blockIdx.x) - a.lead_blocks),
+    __device__ __forceinline__ Row(const RowArgs& a) : Row(a, int64_t(blockIdx.x) - a.lead_blocks) {}
+    __device__ __forceinline__ Row(const RowArgs& a, int64_t row_)
+        : row(row_),
           b(row / a.T),
           t(row - b * a.T),
           x(reinterpret_cast<const E*>(blockIdx.y == 0 ? a.x0 : a.x1) + b * a.sb + t * a.st),
@@ -223,8 +224,7 @@ __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, cons
 // reference's loss NaN through NaN·0; here it is not read at all — DESIGN.md §7.)  Both
 // checks are block-uniform scalar loads ahead of the row; without lengths / mask the
 // launches skip them.
-__device__ __forceinline__ bool pad_row(const RowArgs& a) {
-    const int64_t row = int64_t(blockIdx.x) - a.lead_blocks;
+__device__ __forceinline__ bool pad_row(const RowArgs& a, int64_t row) {
     const int64_t b = row / a.T;
     if (row - b * a.T < a.lengths[b]) return false;
     if (threadIdx.x == 0) {
@@ -270,42 +270,25 @@ __device__ __forceinline__ void masked_row(const RowArgs& a, int64_t row) {
 // LDS (32 KB per workgroup at NL = 4) instead of VGPRs, so a 512-thread workgroup fits in
 // 128 VGPRs and two rows stay in flight per CU (a 201-KB fp32 row held whole in VGPRs
 // needs 1024 threads at ~88 VGPRs: one row per CU, its load / reduce / store phases exposed).
-template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, int WPE = 4>
-__global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
+// One row of the resident kernel (the workgroup's `row`).
+template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL, int WPE>
+__device__ __forceinline__ void vocab_row(const RowArgs& a, int64_t row) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_max2[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     if constexpr (MODE == kFwd) {
-        if (int(blockIdx.x) < a.tail_blocks) {  // the previous step's loss tail (block-uniform branch)
-            __shared__ double tail_red[kMaxThreads / kWave * 16];
-            if (blockIdx.y == 0) loss_tail_block(a.tail, int(blockIdx.x), a.tail_blocks, tail_red);
-            return;
-        }
-    }
-    if constexpr (MODE == kPpo && NL > 0) {  // only the split-residency kernels host it (their VGPR
-                                             // budget is set by the row; the others run it standalone)
-        if (int(blockIdx.x) < a.gae_blocks) {  // the next batch's split GAE (block-uniform branch)
-            __shared__ double gae_red[kMaxThreads / kWave * 8];
-            gae_block<true>(a.gae, int(blockIdx.x), a.gae_blocks, gae_red);
-            return;
-        }
-    }
-    if constexpr (MODE == kFwd) {
-        if (a.lengths && pad_row(a)) return;
+        if (a.lengths && pad_row(a, row)) return;
     }
     if constexpr (MODE == kPpo) {
-        if (a.mask) {
-            const int64_t row = int64_t(blockIdx.x) - a.lead_blocks;
-            if (a.mask[row] == 0) {
-                masked_row<DT>(a, row);
-                return;
-            }
+        if (a.mask && a.mask[row] == 0) {
+            masked_row<DT>(a, row);
+            return;
         }
     }
     typedef typename DT::elem_t E;
     constexpr int EPV = DT::kEPV;
     const int tid = threadIdx.x, nthr = blockDim.x;
-    const Row<DT> r(a);
+    const Row<DT> r(a, row);
     // Row-independent scalars first, computed by thread 0 while the row loads are in
     // flight and parked in LDS (read back after the reductions' barriers): they then
     // occupy no VGPRs beside the row.
@@ -556,6 +539,26 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL 
     }
 }
 
+template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, int WPE = 4>
+__global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
+    if constexpr (MODE == kFwd) {
+        if (int(blockIdx.x) < a.tail_blocks) {  // the previous step's loss tail (block-uniform branch)
+            __shared__ double tail_red[kMaxThreads / kWave * 16];
+            if (blockIdx.y == 0) loss_tail_block(a.tail, int(blockIdx.x), a.tail_blocks, tail_red);
+            return;
+        }
+    }
+    if constexpr (MODE == kPpo && NL > 0) {  // only the split-residency kernels host it (their VGPR
+                                             // budget is set by the row; the others run it standalone)
+        if (int(blockIdx.x) < a.gae_blocks) {  // the next batch's split GAE (block-uniform branch)
+            __shared__ double gae_red[kMaxThreads / kWave * 8];
+            gae_block<true>(a.gae, int(blockIdx.x), a.gae_blocks, gae_red);
+            return;
+        }
+    }
+    vocab_row<DT, NV, MODE, SAME_PHASE, LB512, NL, WPE>(a, int64_t(blockIdx.x) - a.lead_blocks);
+}
+
 // ------------------------------------------------------------------ streaming rows
 // Same arithmetic, but the row is streamed through registers U vectors at a time with an
 // online (max, sum-exp) instead of being held whole: small register footprint => many
@@ -575,7 +578,7 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
     __shared__ float sh_m[kStreamMaxThreads / kWave];
     __shared__ float sh_s[kStreamMaxThreads / kWave];
     if constexpr (MODE == kFwd) {
-        if (a.lengths && pad_row(a)) return;
+        if (a.lengths && pad_row(a, int64_t(blockIdx.x))) return;
     }
     if constexpr (MODE == kPpo) {
         if (a.mask && a.mask[blockIdx.x] == 0) {
@@ -889,12 +892,12 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
             TRLX_ROWS_LAUNCH((k_vocab_rows_stream<DT, 4, MODE>), grid, dim3(thr), stream, a);
         return check_launch("k_vocab_rows_stream");
     }
+    const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
+    const bool lb512 = g.threads <= 512 && (g_resident_lb512 || (MODE == kFwd && g.nv <= 8));
     const dim3 block(g.threads);
     dim3 grid;
     const int rc = rows_grid(a, g.threads, nten, stream, grid, false);
     if (rc) return rc;
-    const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
-    const bool lb512 = g.threads <= 512 && (g_resident_lb512 || (MODE == kFwd && g.nv <= 8));
 #define TRLX_RESIDENT_CASE(N)                                                                          \
     case N:                                                                                           \
         if (same && lb512)                                                                            \
