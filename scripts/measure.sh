@@ -30,7 +30,7 @@ for st in $steps; do
         prof_c4) run ${TAG}_prof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c4 -o run -- $B --config c4 --steps 200 --warmup 5 ;;
         prof_c5) run ${TAG}_prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c5 -o run -- $B --config c5 --steps 100 --warmup 5 ;;
         pmc)
-            for cfg in c2 c4 c5; do
+            for cfg in ${PMC_CFGS:-c2 c3 c4 c5}; do
                 run ${TAG}_pmc_fetch_$cfg 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch_$cfg -o run -- $B --config $cfg --steps 5 --warmup 2 --settle-ms 0 --no-timers
                 run ${TAG}_pmc_write_$cfg 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write_$cfg -o run -- $B --config $cfg --steps 5 --warmup 2 --settle-ms 0 --no-timers
             done ;;
