@@ -73,6 +73,8 @@ const char* trlx_last_error(void);
  *                       for the loss / backward (default), 1 = off, 2 = also for the forward
  *   "split_mid"         mid-length bf16 rows (16k < V <= 32k) in the loss / backward: 0 auto (= 3),
  *                       1 = all in VGPRs, 2 = 5 VGPR + 3 LDS vector steps, 3 = 6 + 2 (8 waves/SIMD)
+ *   "ragged_order"      ragged experience rows with an order scratch: 0 = valid rows first (default),
+ *                       1 = natural order
  *   "store_policy"      gradient-row store cache policy: 0 auto (default: nt; sc1 for all-VGPR rows
  *                       launches writing > 1.5 GB), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
  * Results are identical up to fp32 summation order; only speed changes. */
@@ -94,11 +96,14 @@ int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype,
 /* The experience rows of a ragged batch (decoder lengths [B] int64): a row (b, t) with
  * t >= lengths[b] is store padding — ppo_pipeline.py:47-65 pads each element's logprobs with
  * 0.0 — so its lp is 0 and the row is NOT read (the bytes of a batch of decoder lengths L_b
- * are those of its sum(L_b) tokens).  lengths == NULL: trlx_lsm_gather_fwd. */
+ * are those of its sum(L_b) tokens).  lengths == NULL: trlx_lsm_gather_fwd.  order_ws (or
+ * NULL): trlx_ragged_order_bytes(B, T) bytes of device scratch — a one-workgroup launch
+ * first orders the rows valid-first so the skipped rows do not interleave with them. */
+int64_t trlx_ragged_order_bytes(int64_t B, int64_t T);
 int trlx_lsm_gather_fwd_ragged(const void* x0, const void* x1, int dtype,
                                int64_t B, int64_t T, int64_t V, int64_t sb, int64_t st,
                                const int64_t* labels, int64_t lb, int64_t lt, const int64_t* lengths,
-                               void* out_lp0, void* out_lp1, int out_dtype, void* stream);
+                               void* order_ws, void* out_lp0, void* out_lp1, int out_dtype, void* stream);
 
 /* ---------------------------------------------------------------- A1 backward
  * Autograd of modeling.py:39-40 (log_softmax_backward of the gathered one-hot):
@@ -445,10 +450,10 @@ int trlx_ppo_rollout_loss_ctl(int64_t B, int64_t T, const double* stats, float v
  * Kernels that cannot host it (the streaming rows) run the tail as its own launch first.
  * Stream order is that of the two calls: the tail reads the token records of the loss rows
  * launched before, the GAE tail launched after reads the KL coefficient it updates.
- * lengths: as in trlx_lsm_gather_fwd_ragged (NULL: every row). */
+ * lengths, order_ws: as in trlx_lsm_gather_fwd_ragged (NULL: every row / natural order). */
 int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int64_t B, int64_t T, int64_t V,
                                   int64_t sb, int64_t st, const int64_t* labels, int64_t lb, int64_t lt,
-                                  const int64_t* lengths, void* out_lp0, void* out_lp1, int out_dtype,
+                                  const int64_t* lengths, void* order_ws, void* out_lp0, void* out_lp1, int out_dtype,
                                   int64_t tail_B, int64_t tail_T,
                                   const double* tail_stats, float vf_coef, float* loss, float* loss_stats,
                                   void* workspace, const trlx_kl_ctl* kl, void* stream);

@@ -56,19 +56,31 @@ def _poison(x):
     return d
 
 
-@pytest.mark.parametrize("V,dt", [(32128, torch.bfloat16), (50257, torch.bfloat16), (1031, torch.float32),
-                                  (50257, torch.float32)])
-def test_ragged_experience_rows_not_read(V, dt):
+@pytest.mark.parametrize("V,dt,ordered", [(32128, torch.bfloat16, True), (32128, torch.bfloat16, False),
+                                          (50257, torch.bfloat16, True), (1031, torch.float32, True),
+                                          (1031, torch.float32, False), (50257, torch.float32, True)])
+def test_ragged_experience_rows_not_read(V, dt, ordered):
+    """ordered: with the order scratch (valid rows dispatched first), else natural order."""
     x = _ragged(6, 21, V, 3 + V, dt)
     d = _poison(x)
     B, Tn = 6, 21
     lp0 = torch.full((B, Tn), 7.0, device=DEV)
     lp1 = torch.full((B, Tn), 7.0, device=DEV)
     lg = d["logits"]
+    nb = _lib.query("trlx_ragged_order_bytes", B, Tn)
+    assert nb == 4 * B * Tn
+    order = torch.full((B * Tn,), 12345, dtype=torch.int32, device=DEV) if ordered else None
     _lib.call("trlx_lsm_gather_fwd_ragged", lg.data_ptr(), d["ref_logits"].data_ptr(), _lib.dtype_code(lg), B, Tn, V,
-              lg.stride(0), lg.stride(1), d["labels"].data_ptr(), Tn, 1, d["lengths"].data_ptr(), lp0.data_ptr(),
-              lp1.data_ptr(), _lib.F32, torch.cuda.current_stream().cuda_stream)
+              lg.stride(0), lg.stride(1), d["labels"].data_ptr(), Tn, 1, d["lengths"].data_ptr(),
+              None if order is None else order.data_ptr(), lp0.data_ptr(), lp1.data_ptr(), _lib.F32,
+              torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
+    if order is not None and V == 32128:  # the resident rows took the order: valid rows first, then ~padding
+        L = x["lengths"]
+        nvalid = int(L.sum())
+        want = [b * Tn + t for b in range(B) for t in range(int(L[b]))]
+        want += [~(b * Tn + t) for b in range(B) for t in range(int(L[b]), Tn)]
+        assert order.cpu().tolist() == want and nvalid == len([w for w in want if w >= 0])
     pad = x["pad"]
     for got, src in ((lp0, x["logits"]), (lp1, x["ref_logits"])):
         got = got.cpu()
@@ -94,7 +106,8 @@ def test_ragged_rows_bit_identical_to_dense(V, dt):
         if lens is None:
             _lib.call("trlx_lsm_gather_fwd", *args, lp0.data_ptr(), lp1.data_ptr(), _lib.F32, None, None, s)
         else:
-            _lib.call("trlx_lsm_gather_fwd_ragged", *args, lens.data_ptr(), lp0.data_ptr(), lp1.data_ptr(), _lib.F32, s)
+            _lib.call("trlx_lsm_gather_fwd_ragged", *args, lens.data_ptr(), None, lp0.data_ptr(), lp1.data_ptr(),
+                      _lib.F32, s)
         outs.append((lp0, lp1))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

@@ -4,6 +4,8 @@ different decoder-length patterns, interleaved rounds in one process.
   full    lengths = T, mask all ones (the per-row checks run, nothing is skipped)
   random  bench.py's L ~ U{1..T} (about half the rows skipped)
   sorted  the same lengths sorted descending (the skipped rows gather at the end of the grid)
+  halfB / altB / halfT  fill 0.5: first half of the rollouts valid / every other rollout / the
+          first half of every rollout
 Prints per-launch averages (HIP events) and the step time.
 
   python tools/ragged_probe.py [--config c3] [--steps 60] [--rounds 3]
@@ -21,6 +23,7 @@ def main():
     p.add_argument("--config", default="c3")
     p.add_argument("--steps", type=int, default=60)
     p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--orders", default="0", help="tuning ragged_order values to compare (0 b-major, 1 t-major)")
     a = p.parse_args()
     import torch
     import torch.distributed as dist
@@ -40,15 +43,30 @@ def main():
             "random": (L, (ar < L[:, None]).long())}
     Ls = torch.sort(L, descending=True).values
     pats["sorted"] = (Ls, (ar < Ls[:, None]).long())
-    res = {n: [] for n in pats}
+    # fill 0.5 at three granularities of the padding: whole rollouts (the first half of the
+    # batch valid), alternate rollouts, and the second half of every rollout
+    half = torch.zeros_like(L)
+    half[: B // 2] = T
+    alt = torch.zeros_like(L)
+    alt[::2] = T
+    tail = torch.full_like(L, T // 2)
+    for n, l in (("halfB", half), ("altB", alt), ("halfT", tail)):
+        pats[n] = (l, (ar < l[:, None]).long())
+    from trlx_t5_amd import _lib
+    orders = [int(v) for v in a.orders.split(",")]
+    runs = [(n, o) for n in pats for o in (orders if n != "dense" else orders[:1])]
+    res = {(f"{n} o{o}" if len(orders) > 1 else n): [] for n, o in runs}
     for rnd in range(a.rounds):
-        for key in pats:
-            x["lengths"], x["mask"] = pats[key]
+        for name, o in runs:
+            key = f"{name} o{o}" if len(orders) > 1 else name
+            x["lengths"], x["mask"] = pats[name]
+            _lib.set_tuning("ragged_order", o)
             bench.settle_and_warm(step, torch, ns, dev)
             el, km, _ = bench.timed_run(step, hp, torch, dist, ns, dev, 1, {"experience", "loss"})
             res[key].append((el / a.steps * 1e3, km["experience"] * 1e3, km["loss"] * 1e3))
             print(f"round {rnd} {key:12s} step {res[key][-1][0]:.4f} ms  E {res[key][-1][1]:7.2f} us  "
                   f"L {res[key][-1][2]:7.2f} us", flush=True)
+    _lib.set_tuning("ragged_order", 0)
     fill = float(L.sum()) / (B * T)
     print(f"{a.config} {B}x{T}x{V}: random fill {fill:.4f}")
     for name, r in res.items():

@@ -82,8 +82,9 @@ SIGNATURES = {
     "trlx_set_tuning": (_c_int, [ctypes.c_char_p, _c_i64]),
     "trlx_lsm_gather_fwd": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                      _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
+    "trlx_ragged_order_bytes": (_c_i64, [_c_i64, _c_i64]),
     "trlx_lsm_gather_fwd_ragged": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
-                                            _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
+                                            _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
     "trlx_lsm_gather_bwd": (_c_int, [_c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
                                      _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_i64, _c_i64, _c_vp]),
     "trlx_kl_penalty_rewards": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_f, _c_vp, _c_vp,
@@ -161,8 +162,8 @@ SIGNATURES = {
     "trlx_comm_allreduce_sum_f64": (_c_int, [_c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_comm_destroy": (_c_int, [_c_vp]),
     "trlx_lsm_gather_fwd_loss_tail": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
-                                               _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_vp,
-                                               _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
+                                               _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_i64,
+                                               _c_vp, _c_f, _c_vp, _c_vp, _c_vp, _kl_ctl_p, _c_vp]),
     "trlx_ilql_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_int]),
     "trlx_ilql_prep": (_c_int, [_ilql_p, _c_vp]),
     "trlx_ilql_rows": (_c_int, [_ilql_p, _c_vp]),

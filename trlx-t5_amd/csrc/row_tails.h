@@ -38,6 +38,7 @@ struct Workspace {
     double* gae_rec;
     double* loss_rec;
     float* tokrec;
+    int* order;       // a ragged batch's experience-row dispatch order (vocab_rows.hip k_ragged_order)
 };
 
 // ------------------------------------------------------------------ GAE per rollout

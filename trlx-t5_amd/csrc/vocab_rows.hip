@@ -82,6 +82,10 @@ struct RowArgs {
     float* coef_out;
     // forward rows of a ragged batch: rows (b, t >= lengths[b]) are store padding (pad_row)
     const int64_t* lengths;
+    // ... and their dispatch order (k_ragged_order): workgroup i takes row row_list[i] (>= 0), or
+    // writes the padding row ~row_list[i]; NULL: workgroup i takes row i
+    const int* row_list;
+    int* order_ws;            // host: int32 [B·T] scratch for the order (NULL: natural order)
 };
 
 // ------------------------------------------------------------------ shared row pieces
@@ -224,15 +228,67 @@ __device__ __forceinline__ void token_record(const RowArgs& a, int64_t row, cons
 // reference's loss NaN through NaN·0; here it is not read at all — DESIGN.md §7.)  Both
 // checks are block-uniform scalar loads ahead of the row; without lengths / mask the
 // launches skip them.
-__device__ __forceinline__ bool pad_row(const RowArgs& a, int64_t row) {
-    const int64_t b = row / a.T;
-    if (row - b * a.T < a.lengths[b]) return false;
+__device__ __forceinline__ void pad_write(const RowArgs& a, int64_t row) {
     if (threadIdx.x == 0) {
         st_any(blockIdx.y == 0 ? a.lp0 : a.lp1, a.out_dtype, row, 0.0f);
         float* lse_out = blockIdx.y == 0 ? a.lse0 : a.lse1;
         if (lse_out) lse_out[row] = 0.0f;
     }
+}
+__device__ __forceinline__ bool pad_row(const RowArgs& a, int64_t row) {
+    const int64_t b = row / a.T;
+    if (row - b * a.T < a.lengths[b]) return false;
+    pad_write(a, row);
     return true;
+}
+
+// Dispatch order of a ragged batch's forward rows: the valid rows (b, t < L_b) first, in row
+// order, then the padding rows as ~row.  Measured (tools/ragged_probe.py): the same skipped
+// rows cost ~20 us more at C3 when they are interleaved with the valid rows in dispatch order
+// than when they come after them (a skipped workgroup's short life idles its slot), so the
+// launch that takes its rows in this order pays this one-workgroup launch instead.
+// One workgroup; rollouts in chunks of kOrderThreads (B·T < 2^31).
+constexpr int kOrderThreads = 1024;
+__global__ __launch_bounds__(kOrderThreads) void k_ragged_order(const int64_t* lengths, int B, int T, int* order) {
+    __shared__ int sh[kOrderThreads];
+    __shared__ int s_carry;
+    const int tid = threadIdx.x;
+    // pass 1: the number of valid rows
+    int mine = 0;
+    for (int b = tid; b < B; b += kOrderThreads) mine += int(min(max(lengths[b], int64_t(0)), int64_t(T)));
+    sh[tid] = mine;
+    __syncthreads();
+    for (int s = kOrderThreads / 2; s > 0; s >>= 1) {
+        if (tid < s) sh[tid] += sh[tid + s];
+        __syncthreads();
+    }
+    const int nvalid = sh[0];
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    // pass 2: exclusive scan of the clamped lengths per chunk; rollout b's valid rows go to
+    // [vo, vo + L_b), its padding rows to nvalid + (b·T − vo) onwards
+    for (int b0 = 0; b0 < B; b0 += kOrderThreads) {
+        const int b = b0 + tid;
+        const int Lb = b < B ? int(min(max(lengths[b], int64_t(0)), int64_t(T))) : 0;
+        sh[tid] = Lb;
+        __syncthreads();
+        for (int off = 1; off < kOrderThreads; off <<= 1) {  // inclusive Hillis-Steele scan
+            const int v = tid >= off ? sh[tid - off] : 0;
+            __syncthreads();
+            sh[tid] += v;
+            __syncthreads();
+        }
+        const int vo = s_carry + sh[tid] - Lb;
+        if (b < B) {
+            const int base = b * T;
+            for (int j = 0; j < Lb; ++j) order[vo + j] = base + j;
+            const int po = nvalid + (base - vo);
+            for (int j = Lb; j < T; ++j) order[po + (j - Lb)] = ~(base + j);
+        }
+        __syncthreads();
+        if (tid == kOrderThreads - 1) s_carry += sh[tid];
+        __syncthreads();
+    }
 }
 
 template <class DT>
@@ -277,7 +333,7 @@ __device__ __forceinline__ void vocab_row(const RowArgs& a, int64_t row) {
     __shared__ float sh_max2[kMaxThreads / kWave];
     __shared__ float sh_sum[kMaxThreads / kWave];
     if constexpr (MODE == kFwd) {
-        if (a.lengths && pad_row(a, row)) return;
+        if (a.lengths && !a.row_list && pad_row(a, row)) return;
     }
     if constexpr (MODE == kPpo) {
         if (a.mask && a.mask[row] == 0) {
@@ -556,7 +612,18 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL 
             return;
         }
     }
-    vocab_row<DT, NV, MODE, SAME_PHASE, LB512, NL, WPE>(a, int64_t(blockIdx.x) - a.lead_blocks);
+    int64_t row = int64_t(blockIdx.x) - a.lead_blocks;
+    if constexpr (MODE == kFwd) {
+        if (a.row_list) {  // a ragged batch in valid-rows-first order
+            const int r = a.row_list[row];
+            if (r < 0) {
+                pad_write(a, ~int64_t(r));
+                return;
+            }
+            row = r;
+        }
+    }
+    vocab_row<DT, NV, MODE, SAME_PHASE, LB512, NL, WPE>(a, row);
 }
 
 // ------------------------------------------------------------------ streaming rows
@@ -724,6 +791,7 @@ static thread_local int g_resident_lb512 = 0;    // 1 = <=512-thread rows compil
 static thread_local int g_stream_threads = 0;
 static thread_local int g_stream_unroll = 0;
 static thread_local int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
+static thread_local int g_ragged_order = 0;      // forward rows with lengths: 0 auto (valid rows first), 1 natural
 static thread_local int g_store_pol = 0;         // gradient-row stores: 0 auto, 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
 constexpr double kSC1Bytes = 1.5e9;  // auto: sc1 above this many gradient bytes per launch, else nt
 
@@ -894,6 +962,13 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     }
     const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
     const bool lb512 = g.threads <= 512 && (g_resident_lb512 || (MODE == kFwd && g.nv <= 8));
+    if (MODE == kFwd && a.lengths && a.order_ws && !g_ragged_order) {  // valid rows first
+        hipLaunchKernelGGL(k_ragged_order, dim3(1), dim3(kOrderThreads), 0, stream, a.lengths, int(a.B), int(a.T),
+                           a.order_ws);
+        const int orc = check_launch("k_ragged_order");
+        if (orc) return orc;
+        a.row_list = a.order_ws;
+    }
     const dim3 block(g.threads);
     dim3 grid;
     const int rc = rows_grid(a, g.threads, nten, stream, grid, false);
@@ -948,6 +1023,8 @@ static size_t carve_workspace(void* base, int64_t B, int64_t T, Workspace* w) {
     off += ws_align(sizeof(double) * 16 * size_t(nblk));
     if (w) w->tokrec = reinterpret_cast<float*>(p + off);
     off += ws_align(sizeof(float) * kTokRec * size_t(B * T));
+    if (w) w->order = reinterpret_cast<int*>(p + off);
+    off += ws_align(sizeof(int) * size_t(B * T));
     return off;
 }
 
@@ -971,13 +1048,15 @@ extern "C" int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype, in
     return launch_rows<kFwd>(a, dtype, x1 ? 2 : 1, (hipStream_t)stream);
 }
 
+extern "C" int64_t trlx_ragged_order_bytes(int64_t B, int64_t T) { return 4 * B * T; }
+
 extern "C" int trlx_lsm_gather_fwd_ragged(const void* x0, const void* x1, int dtype, int64_t B, int64_t T,
                                           int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
-                                          int64_t lt, const int64_t* lengths, void* out_lp0, void* out_lp1,
-                                          int out_dtype, void* stream) {
+                                          int64_t lt, const int64_t* lengths, void* order_ws, void* out_lp0,
+                                          void* out_lp1, int out_dtype, void* stream) {
     RowArgs a = {};
     a.x0 = x0; a.x1 = x1; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
-    a.labels = labels; a.lb = lb; a.lt = lt; a.lengths = lengths;
+    a.labels = labels; a.lb = lb; a.lt = lt; a.lengths = lengths; a.order_ws = static_cast<int*>(order_ws);
     a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype;
     if (B * T == 0 && B >= 0 && T >= 0) return TRLX_OK;
     int rc = check_rows(a, dtype);
@@ -992,13 +1071,13 @@ static int fill_loss_tail(LossRolloutArgs* L, int64_t B, int64_t T, const double
 
 extern "C" int trlx_lsm_gather_fwd_loss_tail(const void* x0, const void* x1, int dtype, int64_t B, int64_t T,
                                              int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,
-                                             int64_t lt, const int64_t* lengths, void* out_lp0, void* out_lp1,
-                                             int out_dtype, int64_t tail_B, int64_t tail_T, const double* tail_stats,
-                                             float vf_coef, float* loss, float* loss_stats, void* workspace,
-                                             const trlx_kl_ctl* kl, void* stream) {
+                                             int64_t lt, const int64_t* lengths, void* order_ws, void* out_lp0,
+                                             void* out_lp1, int out_dtype, int64_t tail_B, int64_t tail_T,
+                                             const double* tail_stats, float vf_coef, float* loss, float* loss_stats,
+                                             void* workspace, const trlx_kl_ctl* kl, void* stream) {
     RowArgs a = {};
     a.x0 = x0; a.x1 = x1; a.B = B; a.T = T; a.V = V; a.sb = sb; a.st = st;
-    a.labels = labels; a.lb = lb; a.lt = lt; a.lengths = lengths;
+    a.labels = labels; a.lb = lb; a.lt = lt; a.lengths = lengths; a.order_ws = static_cast<int*>(order_ws);
     a.lp0 = out_lp0; a.lp1 = out_lp1; a.out_dtype = out_dtype;
     int rc = fill_loss_tail(&a.tail, tail_B, tail_T, tail_stats, vf_coef, loss, loss_stats, workspace, kl);
     if (rc) return rc;
@@ -1163,9 +1242,11 @@ extern "C" int trlx_ppo_experience_fused(const void* logits, const void* ref_log
                                          float kl_coef, float gamma, float lam, float* lp, float* ref_lp,
                                          float* rewards, float* adv_raw, void* ret, int ret_dtype,
                                          double* stats, void* workspace, void* stream) {
-    TRLX_REQUIRE(ref_logits, TRLX_ERR_ARG, "NULL reference logits");
-    int rc = trlx_lsm_gather_fwd_ragged(logits, ref_logits, dtype, B, T, V, sb, st, labels, lb, lt, lengths, lp,
-                                        ref_lp, TRLX_F32, stream);
+    TRLX_REQUIRE(ref_logits && workspace, TRLX_ERR_ARG, "NULL reference logits / workspace");
+    Workspace ws;
+    carve_workspace(workspace, B, T, &ws);
+    int rc = trlx_lsm_gather_fwd_ragged(logits, ref_logits, dtype, B, T, V, sb, st, labels, lb, lt, lengths, ws.order,
+                                        lp, ref_lp, TRLX_F32, stream);
     if (rc) return rc;
     return trlx_ppo_rollout_gae(B, T, lp, ref_lp, values, v_dtype, scores, lengths, mask, kl_coef, gamma, lam,
                                 rewards, adv_raw, ret, ret_dtype, stats, workspace, stream);
@@ -1351,6 +1432,9 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
     } else if (k == "split_mid") {
         TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG, "split_mid: 0..3");
         g_split_mid = int(value);
+    } else if (k == "ragged_order") {
+        TRLX_REQUIRE(value == 0 || value == 1, TRLX_ERR_ARG, "ragged_order: 0 (valid rows first) or 1 (natural)");
+        g_ragged_order = int(value);
     } else if (k == "row_order") {
         TRLX_REQUIRE(value == 0 || value == 1, TRLX_ERR_ARG, "row_order: 0 or 1");
         g_row_order = int(value);

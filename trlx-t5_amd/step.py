@@ -157,6 +157,7 @@ class PPOHotPath:
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
         self.timer_names = None  # optional subset of launch names to instrument (None = all)
         self._conv = {}  # int64 buffers for labels / mask / lengths given in another integer dtype
+        self._order_ws = None  # int32 [B*T]: a ragged batch's experience-row order (trlx_lsm_gather_fwd_ragged)
         self._ar_work = None  # pending whitening all-reduce (pipelined schedule)
         self._ar_group = None
         self._lp_bufs = None  # pipelined schedule: two (lp_old, ref_lp) pairs
@@ -325,14 +326,19 @@ class PPOHotPath:
         rows = (logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V, logits.stride(0),
                 logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1))
         outs = (self.lp_old[b0].data_ptr(), self.ref_lp[b0].data_ptr(), _lib.F32)
+        order = None
+        if lengths is not None:  # scratch for the valid-rows-first dispatch order
+            if self._order_ws is None:
+                self._order_ws = torch.empty(self.B * T, dtype=torch.int32, device=self.device)
+            order = self._order_ws.data_ptr()
         if timed:
             self._ev("experience", s)
         if self._tail_pending is not None:  # the previous step's loss tail rides this launch
             pend, self._tail_pending = self._tail_pending, None
-            _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, _lib.ptr(lengths), *outs, *self._tail_args(pend),
+            _lib.call("trlx_lsm_gather_fwd_loss_tail", *rows, _lib.ptr(lengths), order, *outs, *self._tail_args(pend),
                       s.cuda_stream)
         elif lengths is not None:
-            _lib.call("trlx_lsm_gather_fwd_ragged", *rows, lengths.data_ptr(), *outs, s.cuda_stream)
+            _lib.call("trlx_lsm_gather_fwd_ragged", *rows, lengths.data_ptr(), order, *outs, s.cuda_stream)
         else:
             _lib.call("trlx_lsm_gather_fwd", *rows, *outs, None, None, s.cuda_stream)
         if timed:
