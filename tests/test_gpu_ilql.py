@@ -273,3 +273,24 @@ def test_ilql_hot_path_vs_oracle(B, L, V, nq, dtype):
     assert int(tick.abs().sum()) == 0
     with pytest.raises(ValueError):  # head count must match the config
         hp.step(logits.to(DEV), [q.to(DEV) for q in qs[:1]] * (3 - nq), [q.to(DEV) for q in tqs[:1]], vs.to(DEV), bd)
+
+
+@pytest.mark.parametrize("V,dtype", [(50257, torch.float32), (4097, torch.float32), (32128, torch.bfloat16)])
+def test_ilql_zero_weight_rows_not_read(V, dtype):
+    """Rows whose loss weights are all zero — logits rows whose next token is padding
+    (attention_mask[b, t+1] = 0) or the last position, Q rows of terminal actions
+    (dones[b, a] = 0) — have zero gradients and add nothing to the losses: they hold NaN here
+    and every output must still equal the oracle on the clean rows."""
+    B, L = 5, 11
+    logits, qs, tqs, vs, b = make_case(B, L, V, 900 + V, dtype=dtype)
+    A = qs[0].shape[1]
+    lp, qp = logits.clone(), [q.clone() for q in qs]
+    lmask = torch.cat([b.attention_mask[:, 1:] == 0, torch.ones(B, 1, dtype=torch.bool)], dim=1)
+    assert lmask[:, :-1].any() and (b.dones[:, :A] == 0).any()
+    lp[lmask] = float("nan")
+    for q in qp:
+        q[b.dones[:, :A] == 0] = float("nan")
+    got = run_gpu(P.ILQLConfig(), lp, qp, tqs, vs, b)
+    tol = dict(grad_rtol=1e-2, grad_atol=2e-6) if dtype == torch.bfloat16 else {}
+    check(got, run_oracle(logits, qs, tqs, vs, b), **tol)
+    assert torch.equal(got[2][lmask].float(), torch.zeros_like(got[2][lmask].float()))

@@ -143,25 +143,46 @@ __global__ __launch_bounds__(NL ? 512 : kMaxThreads, NL ? 4 : 1) void k_ilql_row
     const E* x;
     E* dx;
     int64_t y;
+    // Rows whose every loss term carries a zero weight have a zero gradient and add nothing to
+    // the sums: the last logits position (logits[:, :-1] only), a logits row whose next token
+    // is padding (AWAC weight attention_mask[b, t+1] = 0, ilql_models.py:98-105) and a Q row of
+    // a terminal action (CQL and TD weights dones[b, a] = 0, :63-74 and :87-96; the V loss of
+    // head 0 too, :76-83).  Such a row is written as zeros without being read (a masked row of
+    // non-finite logits made the reference's loss NaN through NaN·0).  The
+    // per-row mask load runs only when prep found a zero weight (its sums short of the counts).
+    bool skip = id.head < 0 && id.t == a.L - 1;
+    if (!skip) {
+        const double* sums = ilql_sums(a);
+        const bool masked = sums[0] != double(a.B * a.A) || sums[1] != double(a.B * (a.L - 1));
+        if (masked)
+            skip = id.head < 0 ? a.attention_mask[id.b * a.L + id.t + 1] == 0 : a.dones[id.b * S + id.t] == 0;
+    }
     if (id.head < 0) {
         x = static_cast<const E*>(a.logits) + id.b * a.logits_sb + id.t * a.logits_st;
         dx = static_cast<E*>(a.dlogits) + id.b * a.dlogits_sb + id.t * a.dlogits_st;
-        if (id.t == a.L - 1) {  // logits[:, :-1] only: the last position's gradient is 0
-            const RowSplit<DT> s(dx, a.V);
-            const __amdgpu_buffer_rsrc_t rout = make_rsrc(dx + s.head, uint32_t(s.nvec) * 16u);
-            const vec4u z = vec4u_make(0u, 0u, 0u, 0u);
-            for (int i = tid; i < int(s.nvec); i += nthr)
-                __builtin_amdgcn_raw_buffer_store_b128(z, rout, i * 16, 0, kAuxNT);
-            if (tid < s.head) DT::store1(dx, tid, 0.0f);
-            if (tid < s.tail) DT::store1(dx, s.tail0 + tid, 0.0f);
-            if (tid < kIlqlRec) rec[tid] = 0.0f;
-            return;
+    } else {
+        dx = static_cast<E*>(a.dq[id.head]) + id.b * a.dq_sb[id.head] + id.t * a.dq_st[id.head];
+    }
+    if (skip) {
+        const RowSplit<DT> s(dx, a.V);
+        const __amdgpu_buffer_rsrc_t rout = make_rsrc(dx + s.head, uint32_t(s.nvec) * 16u);
+        const vec4u z = vec4u_make(0u, 0u, 0u, 0u);
+        for (int i = tid; i < int(s.nvec); i += nthr)
+            __builtin_amdgcn_raw_buffer_store_b128(z, rout, i * 16, 0, kAuxNT);
+        if (tid < s.head) DT::store1(dx, tid, 0.0f);
+        if (tid < s.tail) DT::store1(dx, s.tail0 + tid, 0.0f);
+        if (tid < kIlqlRec) rec[tid] = 0.0f;
+        if (id.head == 0 && tid == 0) {  // d loss_v / d vs of state (b, t): weight dones[b, t] = 0
+            a.dvs[id.b * S + id.t] = 0.0f;
+            if (id.t == a.A - 1) a.dvs[id.b * S + a.A] = 0.0f;  // V_next is detached
         }
+        return;
+    }
+    if (id.head < 0) {
         y = a.input_ids[id.b * a.L + id.t + 1];
     } else {
         const int h = id.head;
         x = static_cast<const E*>(a.q[h]) + id.b * a.q_sb[h] + id.t * a.q_st[h];
-        dx = static_cast<E*>(a.dq[h]) + id.b * a.dq_sb[h] + id.t * a.dq_st[h];
         const int64_t ix = a.actions_ixs[id.b * a.A + id.t];
         y = (ix >= 0 && ix < a.L - 1) ? a.input_ids[id.b * a.L + 1 + ix] : -1;  // no OOB gather
     }
