@@ -291,6 +291,15 @@ __global__ __launch_bounds__(kOrderThreads) void k_ragged_order(const int64_t* l
     }
 }
 
+// Whether the mask can hold a zero: its sum (the launch's Σmask, one L2-resident scalar) short
+// of B·T.  Only then does every row load its own mask element before its loads (that load
+// cost the C3-shape loss rows ~6 us with an all-ones mask).  A sum that hides zeros behind
+// weights > 1 only skips the skip — the rows are then computed, which is exact too.
+__device__ __forceinline__ bool any_masked(const RowArgs& a) {
+    const double msum = a.msum ? *a.msum : a.msum_host;
+    return msum != double(a.B * a.T);
+}
+
 template <class DT>
 __device__ __forceinline__ void masked_row(const RowArgs& a, int64_t row) {
     typedef typename DT::elem_t E;
@@ -336,7 +345,7 @@ __device__ __forceinline__ void vocab_row(const RowArgs& a, int64_t row) {
         if (a.lengths && !a.row_list && pad_row(a, row)) return;
     }
     if constexpr (MODE == kPpo) {
-        if (a.mask && a.mask[row] == 0) {
+        if (a.mask && any_masked(a) && a.mask[row] == 0) {
             masked_row<DT>(a, row);
             return;
         }
@@ -648,7 +657,7 @@ __global__ __launch_bounds__(kStreamMaxThreads) void k_vocab_rows_stream(RowArgs
         if (a.lengths && pad_row(a, int64_t(blockIdx.x))) return;
     }
     if constexpr (MODE == kPpo) {
-        if (a.mask && a.mask[blockIdx.x] == 0) {
+        if (a.mask && any_masked(a) && a.mask[blockIdx.x] == 0) {
             masked_row<DT>(a, int64_t(blockIdx.x));
             return;
         }
