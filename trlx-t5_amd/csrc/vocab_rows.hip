@@ -335,8 +335,10 @@ __device__ __forceinline__ void masked_row(const RowArgs& a, int64_t row) {
 // LDS (32 KB per workgroup at NL = 4) instead of VGPRs, so a 512-thread workgroup fits in
 // 128 VGPRs and two rows stay in flight per CU (a 201-KB fp32 row held whole in VGPRs
 // needs 1024 threads at ~88 VGPRs: one row per CU, its load / reduce / store phases exposed).
-// One row of the resident kernel (the workgroup's `row`).
-template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL, int WPE>
+// One row of the resident kernel (the workgroup's `row`).  MASKED (loss rows with a mask): the
+// masked-token path is compiled in; the kernels of unmasked launches do not carry it (its
+// inlined code measured 7-11 % slower rows at the C4 strong-scaling shape).
+template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL, int WPE, bool MASKED>
 __device__ __forceinline__ void vocab_row(const RowArgs& a, int64_t row) {
     __shared__ float sh_max[kMaxThreads / kWave];
     __shared__ float sh_max2[kMaxThreads / kWave];
@@ -344,8 +346,8 @@ __device__ __forceinline__ void vocab_row(const RowArgs& a, int64_t row) {
     if constexpr (MODE == kFwd) {
         if (a.lengths && !a.row_list && pad_row(a, row)) return;
     }
-    if constexpr (MODE == kPpo) {
-        if (a.mask && any_masked(a) && a.mask[row] == 0) {
+    if constexpr (MODE == kPpo && MASKED) {
+        if (any_masked(a) && a.mask[row] == 0) {
             masked_row<DT>(a, row);
             return;
         }
@@ -604,7 +606,7 @@ __device__ __forceinline__ void vocab_row(const RowArgs& a, int64_t row) {
     }
 }
 
-template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, int WPE = 4>
+template <class DT, int NV, int MODE, bool SAME_PHASE, bool LB512, int NL = 0, int WPE = 4, bool MASKED = false>
 __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL ? WPE : 1)) void k_vocab_rows(RowArgs a) {
     if constexpr (MODE == kFwd) {
         if (int(blockIdx.x) < a.tail_blocks) {  // the previous step's loss tail (block-uniform branch)
@@ -632,7 +634,7 @@ __global__ __launch_bounds__((LB512 || NL) ? 512 : kMaxThreads, LB512 ? 8 : (NL 
             row = r;
         }
     }
-    vocab_row<DT, NV, MODE, SAME_PHASE, LB512, NL, WPE>(a, row);
+    vocab_row<DT, NV, MODE, SAME_PHASE, LB512, NL, WPE, MASKED>(a, row);
 }
 
 // ------------------------------------------------------------------ streaming rows
@@ -859,6 +861,15 @@ static bool rows_same_phase(const RowArgs& a, size_t es) {
             hipLaunchKernelGGL(KERN, GRID, BLOCK, 0, STREAM, A);                                             \
     } while (0)
 
+// Resident rows launch: loss rows with a mask take the MASKED instantiation.
+#define TRLX_RESIDENT_LAUNCH(DTX, NVX, SPX, LBX, NLX, WPEX, GRID, BLOCK, STREAM, A)                                    \
+    do {                                                                                                         \
+        if (MODE == kPpo && (A).mask)                                                                            \
+            TRLX_ROWS_LAUNCH((k_vocab_rows<DTX, NVX, MODE, SPX, LBX, NLX, WPEX, MODE == kPpo>), GRID, BLOCK, STREAM, A); \
+        else                                                                                                     \
+            TRLX_ROWS_LAUNCH((k_vocab_rows<DTX, NVX, MODE, SPX, LBX, NLX, WPEX, false>), GRID, BLOCK, STREAM, A);  \
+    } while (0)
+
 // Work folded in ahead of the rows that a kernel cannot host runs as its own launch first:
 // the loss tail (any resident kernel hosts it), the split GAE (hosted by workgroups of at
 // least kRolloutThreads threads; never by the streaming rows).
@@ -909,9 +920,9 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
             const int rc = rows_grid(a, 512, nten, stream, grid, true);
             if (rc) return rc;
             if (MODE == kFwd || rows_same_phase(a, 2))
-                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 9, MODE, true, false, 4, 6>), grid, dim3(512), stream, a);
+                TRLX_RESIDENT_LAUNCH(DT, 9, true, false, 4, 6, grid, dim3(512), stream, a);
             else
-                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 9, MODE, false, false, 4, 6>), grid, dim3(512), stream, a);
+                TRLX_RESIDENT_LAUNCH(DT, 9, false, false, 4, 6, grid, dim3(512), stream, a);
             return check_launch("k_vocab_rows (split LDS, bf16)");
         }
         // mid-length bf16 rows (V 16k-32k, T5/UL2's 32128) in the loss / backward: the last
@@ -928,9 +939,9 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
             const int rc = rows_grid(a, 512, nten, stream, grid, true);
             if (rc) return rc;
             if (sm == 3)
-                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 6, MODE, true, false, 2, 8>), grid, dim3(512), stream, a);
+                TRLX_RESIDENT_LAUNCH(DT, 6, true, false, 2, 8, grid, dim3(512), stream, a);
             else
-                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 5, MODE, true, false, 3, 8>), grid, dim3(512), stream, a);
+                TRLX_RESIDENT_LAUNCH(DT, 5, true, false, 3, 8, grid, dim3(512), stream, a);
             return check_launch("k_vocab_rows (split LDS, mid bf16)");
         }
     }
@@ -943,9 +954,9 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
             const int rc = rows_grid(a, 512, nten, stream, grid, true);
             if (rc) return rc;
             if (MODE == kFwd || rows_same_phase(a, 4))
-                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 21, MODE, true, false, 4>), grid, dim3(512), stream, a);
+                TRLX_RESIDENT_LAUNCH(DT, 21, true, false, 4, 4, grid, dim3(512), stream, a);
             else
-                TRLX_ROWS_LAUNCH((k_vocab_rows<DT, 21, MODE, false, false, 4>), grid, dim3(512), stream, a);
+                TRLX_RESIDENT_LAUNCH(DT, 21, false, false, 4, 4, grid, dim3(512), stream, a);
             return check_launch("k_vocab_rows (split LDS)");
         }
     }
@@ -985,11 +996,11 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
 #define TRLX_RESIDENT_CASE(N)                                                                          \
     case N:                                                                                           \
         if (same && lb512)                                                                            \
-            TRLX_ROWS_LAUNCH((k_vocab_rows<DT, N, MODE, true, true>), grid, block, stream, a);   \
+            TRLX_RESIDENT_LAUNCH(DT, N, true, true, 0, 4, grid, block, stream, a);   \
         else if (same)                                                                                \
-            TRLX_ROWS_LAUNCH((k_vocab_rows<DT, N, MODE, true, false>), grid, block, stream, a);  \
+            TRLX_RESIDENT_LAUNCH(DT, N, true, false, 0, 4, grid, block, stream, a);  \
         else                                                                                          \
-            TRLX_ROWS_LAUNCH((k_vocab_rows<DT, N, MODE, MODE == kFwd, false>), grid, block, stream, a); \
+            TRLX_RESIDENT_LAUNCH(DT, N, MODE == kFwd, false, 0, 4, grid, block, stream, a); \
         break;
     switch (g.nv) {
         TRLX_RESIDENT_CASE(1) TRLX_RESIDENT_CASE(2) TRLX_RESIDENT_CASE(3) TRLX_RESIDENT_CASE(4)
