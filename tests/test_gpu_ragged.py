@@ -217,3 +217,46 @@ def test_ragged_pipeline_matches_step():
             assert torch.equal(a, b)
         assert bool(torch.isfinite(g[0]).all()) and bool(torch.isfinite(g[2].float()).all())
 
+
+
+def test_fused_abi_ragged_step():
+    """The fused C-ABI pair (trlx_ppo_experience_fused with lengths — its experience rows
+    ordered valid-first through the workspace — and trlx_ppo_loss_fused with the mask) on a
+    poisoned ragged batch vs the oracle on the clean one."""
+    B, Tn, V = 12, 40, 32128
+    x = _ragged(B, Tn, V, 321)
+    d = _poison(x)
+    s = torch.cuda.current_stream().cuda_stream
+    f32 = dict(dtype=torch.float32, device=DEV)
+    lp, rlp, rew, adv, ret = (torch.empty(B, Tn, **f32) for _ in range(5))
+    lpn, dv = torch.empty(B, Tn, **f32), torch.empty(B, Tn, **f32)
+    stats = torch.zeros(_lib.MOMENT_SLOTS, dtype=torch.float64, device=DEV)
+    loss, lstats = torch.empty(1, **f32), torch.empty(_lib.PPO_STATS, **f32)
+    ws = torch.zeros(_lib.query("trlx_ppo_workspace_bytes", B, Tn), dtype=torch.uint8, device=DEV)
+    dx = torch.empty(B, Tn, V, dtype=torch.bfloat16, device=DEV)
+    lg, rg, ng = d["logits"], d["ref_logits"], d["new_logits"]
+    y = d["labels"]
+    _lib.call("trlx_ppo_experience_fused", lg.data_ptr(), rg.data_ptr(), _lib.BF16, B, Tn, V, Tn * V, V, y.data_ptr(),
+              Tn, 1, d["old_values"].data_ptr(), _lib.F32, d["scores"].data_ptr(), d["lengths"].data_ptr(),
+              d["mask"].data_ptr(), 0.05, 1.0, 0.95, lp.data_ptr(), rlp.data_ptr(), rew.data_ptr(), adv.data_ptr(),
+              ret.data_ptr(), _lib.F32, stats.data_ptr(), ws.data_ptr(), s)
+    _lib.call("trlx_ppo_loss_fused", ng.data_ptr(), _lib.BF16, B, Tn, V, Tn * V, V, y.data_ptr(), Tn, 1, lp.data_ptr(),
+              _lib.F32, adv.data_ptr(), stats.data_ptr(), 1, d["mask"].data_ptr(), d["values"].data_ptr(), _lib.F32,
+              d["old_values"].data_ptr(), _lib.F32, ret.data_ptr(), _lib.F32, 0.2, 0.2, 1.0, lpn.data_ptr(),
+              dx.data_ptr(), Tn * V, V, dv.data_ptr(), loss.data_ptr(), lstats.data_ptr(), ws.data_ptr(), s)
+    torch.cuda.synchronize()
+    ref = orc.ppo_step_reference(x["logits"].float(), x["ref_logits"].float(), x["new_logits"].float(), x["labels"],
+                                 x["old_values"], x["values"], x["scores"], kl_coef=0.05, lengths=x["lengths"],
+                                 mask=x["mask"])
+    torch.testing.assert_close(lp.cpu(), ref["lp"], **RT32)
+    torch.testing.assert_close(rlp.cpu(), ref["ref_lp"], **RT32)
+    torch.testing.assert_close(rew.cpu(), ref["rewards"], **RT32)
+    torch.testing.assert_close(ret.cpu(), ref["returns"], rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(lpn.cpu(), loss_rows_lp(ref["new_lp"], x["mask"]), **RT32)
+    torch.testing.assert_close(loss.cpu().reshape(()), ref["loss"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dv.cpu(), ref["dvalues"], rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(dx.float().cpu(), ref["dlogits"], rtol=8e-3, atol=1e-9)
+    st = lstats.cpu().tolist()
+    for i, k in enumerate(P.STATS_KEYS):
+        assert st[i] == pytest.approx(float(ref["stats"][k]), rel=1e-5, abs=1e-6), k
+    assert int(x["lengths"].sum()) < B * Tn  # a ragged batch
