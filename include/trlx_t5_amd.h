@@ -98,7 +98,8 @@ int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype,
  * 0.0 — so its lp is 0 and the row is NOT read (the bytes of a batch of decoder lengths L_b
  * are those of its sum(L_b) tokens).  lengths == NULL: trlx_lsm_gather_fwd.  order_ws (or
  * NULL): trlx_ragged_order_bytes(B, T) bytes of device scratch — a one-workgroup launch
- * first orders the rows valid-first so the skipped rows do not interleave with them. */
+ * first orders the rows valid-first so the skipped rows do not interleave with them (the
+ * scratch then holds the B·T row ids, valid first and ~id for the padding, and the count). */
 int64_t trlx_ragged_order_bytes(int64_t B, int64_t T);
 int trlx_lsm_gather_fwd_ragged(const void* x0, const void* x1, int dtype,
                                int64_t B, int64_t T, int64_t V, int64_t sb, int64_t st,
@@ -327,6 +328,16 @@ int trlx_lmhead_set_variant(int variant);
 int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                          int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
                          int lp_dtype, float* lse_out, void* workspace, void* stream);
+/* The same over a ragged batch: N = B·T tokens in rollouts of T, decoder lengths [B] int64.
+ * Tokens past their rollout's length are store padding: lp (and lse) 0 there.  With an order
+ * scratch (trlx_ragged_order_bytes(B, T) bytes) the 128 x 256 MFMA tiles (the H <= 1024,
+ * N >= 2048 variant) gather the valid tokens' hidden rows and skip the padding's tiles — the
+ * GEMM work of a batch of decoder lengths L_b is that of its sum(L_b) tokens; the other
+ * variants compute every token and zero the padding's lp.  N·ldh·2 must stay below 2 GB. */
+int trlx_lmhead_logprobs_ragged(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
+                                int64_t H, int64_t V, const int64_t* labels, int64_t lb, const int64_t* lengths,
+                                int64_t T, void* order_ws, void* lp_out, int lp_dtype, float* lse_out,
+                                void* workspace, void* stream);
 
 /* ---------------------------------------------------------------- §8f rank 3: ILQL sampling step
  * One decode step of CausalLMWithValueHeads.generate (ilql_models.py:296-316) per row b:

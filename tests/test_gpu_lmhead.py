@@ -234,3 +234,86 @@ def test_experience_from_hidden_route_arguments():
     h32 = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.float32, DEV, kl_coef=0.05)
     with pytest.raises(ValueError):
         h32.experience_from_hidden(h, w, h, w, y, ov, sc, route="gemm")
+
+
+def _ragged_lmhead(h, w, y, B, T, L, variant):
+    from trlx_t5_amd import _lib
+    N, H = h.shape
+    V = w.shape[0]
+    lp = torch.full((N,), 7.0, device=DEV)
+    lse = torch.full((N,), 7.0, device=DEV)
+    ws = torch.empty(_lib.query("trlx_lmhead_workspace_bytes", N, V), dtype=torch.uint8, device=DEV)
+    order = torch.empty(_lib.query("trlx_ragged_order_bytes", B, T), dtype=torch.uint8, device=DEV)
+    _lib.call("trlx_lmhead_set_variant", variant)
+    try:
+        _lib.call("trlx_lmhead_logprobs_ragged", h.data_ptr(), H, w.data_ptr(), H, N, H, V, y.data_ptr(), 1,
+                  L.data_ptr(), T, order.data_ptr(), lp.data_ptr(), _lib.F32, lse.data_ptr(), ws.data_ptr(),
+                  torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("trlx_lmhead_set_variant", 0)
+    return lp.cpu(), lse.cpu()
+
+
+@pytest.mark.parametrize("variant,B,T,H", [(9, 64, 48, 768), (9, 37, 70, 256), (8, 64, 48, 768), (3, 9, 20, 128)])
+def test_lmhead_ragged(variant, B, T, H):
+    """trlx_lmhead_logprobs_ragged: tokens past their rollout's decoder length give lp = lse = 0
+    (their hidden rows hold NaN: variant 9 gathers only the valid rows and skips the padding's
+    tiles; the others compute every token and zero the padding); the valid tokens carry the
+    dense launch's exact bits."""
+    V = 1031
+    g = torch.Generator().manual_seed(B * T + variant)
+    h = (torch.randn(B * T, H, generator=g) * 0.2).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * 0.2).to(torch.bfloat16)
+    y = torch.randint(0, V, (B * T,), generator=g)
+    L = torch.randint(1, T + 1, (B,), generator=g)
+    L[0] = T
+    pad = (torch.arange(T)[None, :] >= L[:, None]).reshape(-1)
+    hd, wd, yd = h.to(DEV), w.to(DEV), y.to(DEV)
+    from trlx_t5_amd import _lib
+    _lib.call("trlx_lmhead_set_variant", variant)
+    try:
+        dense, dlse = P.lm_head_logprobs(hd, wd, yd, out_dtype=torch.float32, return_lse=True)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("trlx_lmhead_set_variant", 0)
+    hp = hd.clone()
+    if variant == 9:
+        hp[pad.to(DEV)] = float("nan")
+    lp, lse = _ragged_lmhead(hp, wd, yd, B, T, L.to(DEV), variant)
+    assert torch.equal(lp[pad], torch.zeros(int(pad.sum()))) and torch.equal(lse[pad], torch.zeros(int(pad.sum())))
+    assert torch.equal(lp[~pad], dense.cpu()[~pad]) and torch.equal(lse[~pad], dlse.cpu()[~pad])
+    torch.testing.assert_close(lp[~pad].double(), oracle_lp(h[~pad], w, y[~pad]), rtol=1e-5, atol=1e-4)
+
+
+def test_experience_from_hidden_ragged():
+    """experience_from_hidden (fused route) with decoder lengths: lp / ref_lp 0 past each
+    length, equal to the dense route elsewhere; rewards / returns as the oracle's padded store."""
+    B, T, H, V = 64, 48, 256, 1031
+    g = torch.Generator().manual_seed(5)
+    h = (torch.randn(B, T, H, generator=g) * 0.2).to(torch.bfloat16)
+    hr = (h.float() + 0.02 * torch.randn(B, T, H, generator=g)).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * 0.2).to(torch.bfloat16)
+    y = torch.randint(0, V, (B, T), generator=g)
+    ov = torch.randn(B, T, generator=g)
+    sc = torch.randn(B, generator=g)
+    L = torch.randint(1, T + 1, (B,), generator=g)
+    pad = torch.arange(T)[None, :] >= L[:, None]
+    ov = ov.masked_fill(pad, 0)
+    d = lambda t: t.to(DEV)  # noqa: E731
+    outs = []
+    for lens in (None, d(L)):
+        hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+        hp.experience_from_hidden(d(h), d(w), d(hr), d(w), d(y), d(ov), d(sc), lengths=lens, route="fused")
+        torch.cuda.synchronize()
+        outs.append((hp.lp_old.cpu().clone(), hp.ref_lp.cpu().clone(), hp.rewards.cpu().clone(),
+                     hp.returns.cpu().clone()))
+    (lp0, rlp0, _, _), (lp1, rlp1, rew1, ret1) = outs
+    assert torch.equal(lp1[pad], torch.zeros(int(pad.sum()))) and torch.equal(rlp1[pad], torch.zeros(int(pad.sum())))
+    assert torch.equal(lp1[~pad], lp0[~pad]) and torch.equal(rlp1[~pad], rlp0[~pad])
+    logits = h.double() @ w.double().t()
+    rlogits = hr.double() @ w.double().t()
+    ref = orc.ppo_step_reference(logits, rlogits, logits, y, ov, ov, sc, kl_coef=0.05, lengths=L,
+                                 mask=(~pad).long())
+    torch.testing.assert_close(rew1.double(), ref["rewards"], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(ret1.double(), ref["returns"].double(), rtol=1e-4, atol=1e-4)

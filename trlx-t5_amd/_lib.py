@@ -127,6 +127,8 @@ SIGNATURES = {
     "trlx_lmhead_set_variant": (_c_int, [_c_int]),
     "trlx_lmhead_logprobs": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp,
                                       _c_int, _c_vp, _c_vp, _c_vp]),
+    "trlx_lmhead_logprobs_ragged": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
+                                             _c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
     "trlx_ilql_sample": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_i64, _c_vp,
                                   _c_i64, _c_i64, _c_f, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_rows_copy": (_c_int, [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp,

@@ -57,6 +57,15 @@ struct LmHeadArgs {
     float2* part;          // [N, nvt] (max, Σexp) per vocab tile
     float* xlab;           // [N] label logit
     int nvt;
+    // a ragged batch (N = B·T tokens, rollouts of T): `rows` = k_ragged_order's list (the valid
+    // tokens first, then ~token of the padding), `nrows` its count.  The s2 tiles take token
+    // m < *nrows as rows[m] and tiles past the count exit; the combine writes lp = 0 for the
+    // padding.  Without rows but with lengths (the other variants): every token computed,
+    // the padding's lp written as 0 by the combine.
+    const int* rows;
+    const int* nrows;
+    const int64_t* lengths;
+    int T;
 };
 
 // Swizzled LDS image of a [rows][64 k] bf16 tile: row r is 128 B; its 16-B chunk c sits at
@@ -450,20 +459,29 @@ __device__ __forceinline__ bf16x8_t s2_frag(const char* tile, int r, int c) {
     return *reinterpret_cast<const bf16x8_t*>(tile + r * 64 + s2_chunk(r, c) * 16);
 }
 
+// RAGGED: token m of the tile grid is row rows[m] of a ragged batch, m < *nrows (the valid
+// tokens, k_ragged_order); tiles past the count exit at once, so padding costs no MFMA work.
+template <bool RAGGED>
 __global__ __launch_bounds__(256, 2) void k_lmhead_s2(LmHeadArgs a) {
     typedef LmS2 G;
     __shared__ __attribute__((aligned(16))) char smem[kS2Lds];  // ONE LDS object (glds waits)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int ntt = (a.N + G::BM - 1) / G::BM;
+    const int nv = RAGGED ? *a.nrows : a.N;  // tokens of the grid (block-uniform)
+    if (RAGGED && nv == 0) return;
+    // token tiles fastest (the weight tile stays in L2 across them); ragged: over the valid
+    // tokens' tiles only, so the grid's surplus blocks are its last ones (they exit at once —
+    // interleaved with working ones they would idle CU slots, vocab_rows.hip k_ragged_order)
+    const int ntt = ((RAGGED ? nv : a.N) + G::BM - 1) / G::BM;
     const int b = blockIdx.x;
     const int mt = b % ntt, vt = b / ntt;
+    if (RAGGED && vt >= a.nvt) return;
     const int m0 = mt * G::BM, n0 = vt * G::BN;
     float2* cmb = reinterpret_cast<float2*>(smem + 3 * kS2Stage);
     int* lab = reinterpret_cast<int*>(smem + 3 * kS2Stage + 2 * G::BM * 8);
     if (tid < G::BM) {  // before any LDS DMA: an ordinary load later would drain them (vmcnt(0))
         const int m = m0 + tid;
-        lab[tid] = m < a.N ? int(a.labels[int64_t(m) * a.lb]) : -1;
+        lab[tid] = m < nv ? int(a.labels[int64_t(RAGGED ? a.rows[m] : m) * a.lb]) : -1;
     }
     // DMA groups: 16 rows x 64 B per wave instruction; groups 0..7 = the A tile (tokens),
     // 8..23 = the B tile (vocab); wave w issues groups w, w+4, ..., w+20.  Lane l -> row
@@ -473,15 +491,18 @@ __global__ __launch_bounds__(256, 2) void k_lmhead_s2(LmHeadArgs a) {
     // DMA.
     const int rl = lane >> 2;
     const int lc = (lane & 3) ^ ((lane >> 4) & 3);
-    const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.h + int64_t(m0) * a.ldh, 0x7ffffff0u);
+    // (RAGGED: the A rows are gathered — the resource starts at token 0, each lane's offset
+    // is its token's row; the host checks N·ldh·2 < 2^31)
+    const __amdgpu_buffer_rsrc_t rA = make_rsrc(a.h + (RAGGED ? int64_t(0) : int64_t(m0) * a.ldh), 0x7ffffff0u);
     const __amdgpu_buffer_rsrc_t rB = make_rsrc(a.w + int64_t(n0) * a.ldw, 0x7ffffff0u);
     int voff[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const int g = i * 4 + wave;
         if (i < 2) {
-            const int r = min(g * 16 + rl, a.N - 1 - m0);
-            voff[i] = (r * int(a.ldh) + lc * 8) * 2;
+            const int r = min(g * 16 + rl, nv - 1 - m0);
+            const int row = RAGGED ? a.rows[m0 + r] : r;
+            voff[i] = (row * int(a.ldh) + lc * 8) * 2;
         } else {
             const int r = min((g - 8) * 16 + rl, a.V - 1 - n0);
             voff[i] = (r * int(a.ldw) + lc * 8) * 2;
@@ -558,7 +579,7 @@ __global__ __launch_bounds__(256, 2) void k_lmhead_s2(LmHeadArgs a) {
             sm = row16_sum(sm);
             if (cl == 0) cmb[wc * G::BM + rt] = make_float2(mx, sm);
             const int dy = lab[rt] - (n0 + wc * G::kWCols);
-            if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < a.N) {
+            if (dy >= 0 && dy < G::kWCols && (dy & 15) == cl && m0 + rt < nv) {
                 float xy = x[0];
 #pragma unroll
                 for (int j = 1; j < G::kNR; ++j) xy = (dy >> 4) == j ? x[j] : xy;
@@ -568,7 +589,7 @@ __global__ __launch_bounds__(256, 2) void k_lmhead_s2(LmHeadArgs a) {
     }
     __syncthreads();
     for (int t = tid; t < G::BM; t += G::kThreads) {
-        if (m0 + t >= a.N) continue;
+        if (m0 + t >= nv) continue;
         float m = -INFINITY;
 #pragma unroll
         for (int c = 0; c < G::WN; ++c) m = fmaxf(m, cmb[c * G::BM + t].x);
@@ -587,8 +608,24 @@ __global__ __launch_bounds__(256, 2) void k_lmhead_s2(LmHeadArgs a) {
 // One wave per token: merge the nvt partials (fixed order per lane, then a fixed butterfly).
 __global__ __launch_bounds__(256) void k_lmhead_combine(LmHeadArgs a, void* lp, int lp_dtype, float* lse_out) {
     const int lane = threadIdx.x & 63;
-    const int64_t n = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    const int64_t n = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);  // partials index
     if (n >= a.N) return;
+    int64_t tok = n;  // output token
+    bool pad = false;
+    if (a.rows) {  // compact index n: valid token rows[n], or the padding token ~rows[n]
+        const int r = a.rows[n];
+        pad = n >= *a.nrows;
+        tok = pad ? ~int64_t(r) : int64_t(r);
+    } else if (a.lengths) {
+        pad = n % a.T >= a.lengths[n / a.T];
+    }
+    if (pad) {  // the padded store's 0.0 (ppo_pipeline.py:47-65)
+        if (lane == 0) {
+            st_any(lp, lp_dtype, tok, 0.0f);
+            if (lse_out) lse_out[tok] = 0.0f;
+        }
+        return;
+    }
     const float2* p = a.part + n * a.nvt;
     float m = -INFINITY, s = 0.f;
     for (int t = lane; t < a.nvt; t += kWave) {
@@ -607,13 +644,13 @@ __global__ __launch_bounds__(256) void k_lmhead_combine(LmHeadArgs a, void* lp, 
                 (m2 == -INFINITY ? 0.f : s2 * exp2_fast((m2 - nm) * kLog2e));
         m = nm;
     }
-    const int64_t y = a.labels[n * a.lb];
+    const int64_t y = a.labels[tok * a.lb];
     const bool y_ok = y >= 0 && y < a.V;
     if (lane == 0) {
         const float lse = m + logf(s);
         const float lpv = y_ok ? a.xlab[n] - lse : NAN;  // label logit picked out by the tile kernel
-        st_any(lp, lp_dtype, n, lpv);
-        if (lse_out) lse_out[n] = lse;
+        st_any(lp, lp_dtype, tok, lpv);
+        if (lse_out) lse_out[tok] = lse;
     }
 }
 
@@ -662,7 +699,10 @@ static int lm_launch_s2(const LmHeadArgs& a, hipStream_t stream) {
     const int64_t ntt = (a.N + LmS2::BM - 1) / LmS2::BM;
     TRLX_REQUIRE(ntt * a.nvt < (int64_t(1) << 31), TRLX_ERR_SHAPE, "too many tiles");
     TRLX_REQUIRE(a.H % kS2BK == 0, TRLX_ERR_SHAPE, "hidden size must be a multiple of %d", kS2BK);
-    hipLaunchKernelGGL(k_lmhead_s2, dim3(unsigned(ntt * a.nvt)), dim3(256), 0, stream, a);
+    if (a.rows)
+        hipLaunchKernelGGL(k_lmhead_s2<true>, dim3(unsigned(ntt * a.nvt)), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(k_lmhead_s2<false>, dim3(unsigned(ntt * a.nvt)), dim3(256), 0, stream, a);
     return check_launch("k_lmhead_s2");
 }
 
@@ -673,9 +713,9 @@ static int lm_launch_pp2(const LmHeadArgs& a, hipStream_t stream) {
     return check_launch("k_lmhead_pp2");
 }
 
-extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
-                                    int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
-                                    int lp_dtype, float* lse_out, void* workspace, void* stream) {
+static int lmhead_impl(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N, int64_t H,
+                       int64_t V, const int64_t* labels, int64_t lb, const int64_t* lengths, int64_t T, void* order_ws,
+                       void* lp_out, int lp_dtype, float* lse_out, void* workspace, void* stream) {
     TRLX_REQUIRE(hidden && weight && labels && lp_out && workspace, TRLX_ERR_ARG, "NULL argument");
     TRLX_REQUIRE(N >= 0 && V > 0 && H > 0, TRLX_ERR_SHAPE, "bad shape N=%lld H=%lld V=%lld", (long long)N,
                  (long long)H, (long long)V);
@@ -702,6 +742,19 @@ extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void*
     a.part = static_cast<float2*>(workspace);
     a.xlab = reinterpret_cast<float*>(static_cast<char*>(workspace) + N * a.nvt * int64_t(sizeof(float2)));
     const int var = lm_variant(N, H);
+    if (lengths) {
+        TRLX_REQUIRE(T > 0 && N % T == 0, TRLX_ERR_SHAPE, "ragged lm_head: N = %lld is not B x T = %lld",
+                     (long long)N, (long long)T);
+        a.lengths = lengths;
+        a.T = int(T);
+        if (var == 9 && order_ws) {  // the s2 tiles take the valid tokens only
+            TRLX_REQUIRE(N * ldh * 2 < (int64_t(1) << 31), TRLX_ERR_SHAPE, "ragged lm_head: hidden rows span >= 2 GB");
+            const int orc = launch_ragged_order(lengths, N / T, T, static_cast<int*>(order_ws), (hipStream_t)stream);
+            if (orc) return orc;
+            a.rows = static_cast<const int*>(order_ws);
+            a.nrows = a.rows + N;
+        }
+    }
     const int rc = var == 8   ? lm_launch_pp2(a, (hipStream_t)stream)
                    : var == 9 ? lm_launch_s2(a, (hipStream_t)stream)
                               : lm_launch_small(a, (hipStream_t)stream);
@@ -709,4 +762,19 @@ extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void*
     hipLaunchKernelGGL(k_lmhead_combine, dim3(unsigned((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a, lp_out,
                        lp_dtype, lse_out);
     return check_launch("k_lmhead_combine");
+}
+
+extern "C" int trlx_lmhead_logprobs(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
+                                    int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
+                                    int lp_dtype, float* lse_out, void* workspace, void* stream) {
+    return lmhead_impl(hidden, ldh, weight, ldw, N, H, V, labels, lb, nullptr, 0, nullptr, lp_out, lp_dtype, lse_out,
+                       workspace, stream);
+}
+
+extern "C" int trlx_lmhead_logprobs_ragged(const void* hidden, int64_t ldh, const void* weight, int64_t ldw,
+                                           int64_t N, int64_t H, int64_t V, const int64_t* labels, int64_t lb,
+                                           const int64_t* lengths, int64_t T, void* order_ws, void* lp_out,
+                                           int lp_dtype, float* lse_out, void* workspace, void* stream) {
+    return lmhead_impl(hidden, ldh, weight, ldw, N, H, V, labels, lb, lengths, T, order_ws, lp_out, lp_dtype, lse_out,
+                       workspace, stream);
 }

@@ -249,7 +249,8 @@ __device__ __forceinline__ bool pad_row(const RowArgs& a, int64_t row) {
 // launch that takes its rows in this order pays this one-workgroup launch instead.
 // One workgroup; rollouts in chunks of kOrderThreads (B·T < 2^31).
 constexpr int kOrderThreads = 1024;
-__global__ __launch_bounds__(kOrderThreads) void k_ragged_order(const int64_t* lengths, int B, int T, int* order) {
+__global__ __launch_bounds__(kOrderThreads) void k_ragged_order(const int64_t* lengths, int B, int T, int* order,
+                                                                int* count) {
     __shared__ int sh[kOrderThreads];
     __shared__ int s_carry;
     const int tid = threadIdx.x;
@@ -263,7 +264,10 @@ __global__ __launch_bounds__(kOrderThreads) void k_ragged_order(const int64_t* l
         __syncthreads();
     }
     const int nvalid = sh[0];
-    if (tid == 0) s_carry = 0;
+    if (tid == 0) {
+        s_carry = 0;
+        *count = nvalid;  // after the list (order scratch: trlx_ragged_order_bytes)
+    }
     __syncthreads();
     // pass 2: exclusive scan of the clamped lengths per chunk; rollout b's valid rows go to
     // [vo, vo + L_b), its padding rows to nvalid + (b·T − vo) onwards
@@ -983,9 +987,7 @@ static int launch_rows_dt(const RowArgs& a0, int nten, hipStream_t stream) {
     const bool same = MODE == kFwd || rows_same_phase(a, sizeof(typename DT::elem_t));
     const bool lb512 = g.threads <= 512 && (g_resident_lb512 || (MODE == kFwd && g.nv <= 8));
     if (MODE == kFwd && a.lengths && a.order_ws && !g_ragged_order) {  // valid rows first
-        hipLaunchKernelGGL(k_ragged_order, dim3(1), dim3(kOrderThreads), 0, stream, a.lengths, int(a.B), int(a.T),
-                           a.order_ws);
-        const int orc = check_launch("k_ragged_order");
+        const int orc = launch_ragged_order(a.lengths, a.B, a.T, a.order_ws, stream);
         if (orc) return orc;
         a.row_list = a.order_ws;
     }
@@ -1044,8 +1046,14 @@ static size_t carve_workspace(void* base, int64_t B, int64_t T, Workspace* w) {
     if (w) w->tokrec = reinterpret_cast<float*>(p + off);
     off += ws_align(sizeof(float) * kTokRec * size_t(B * T));
     if (w) w->order = reinterpret_cast<int*>(p + off);
-    off += ws_align(sizeof(int) * size_t(B * T));
+    off += ws_align(size_t(ragged_order_bytes(B, T)));
     return off;
+}
+
+int launch_ragged_order(const int64_t* lengths, int64_t B, int64_t T, int* order, hipStream_t stream) {
+    hipLaunchKernelGGL(k_ragged_order, dim3(1), dim3(kOrderThreads), 0, stream, lengths, int(B), int(T), order,
+                       order + B * T);
+    return check_launch("k_ragged_order");
 }
 
 }  // namespace trlx
@@ -1068,7 +1076,7 @@ extern "C" int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype, in
     return launch_rows<kFwd>(a, dtype, x1 ? 2 : 1, (hipStream_t)stream);
 }
 
-extern "C" int64_t trlx_ragged_order_bytes(int64_t B, int64_t T) { return 4 * B * T; }
+extern "C" int64_t trlx_ragged_order_bytes(int64_t B, int64_t T) { return ragged_order_bytes(B, T); }
 
 extern "C" int trlx_lsm_gather_fwd_ragged(const void* x0, const void* x1, int dtype, int64_t B, int64_t T,
                                           int64_t V, int64_t sb, int64_t st, const int64_t* labels, int64_t lb,

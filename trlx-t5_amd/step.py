@@ -157,7 +157,7 @@ class PPOHotPath:
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
         self.timer_names = None  # optional subset of launch names to instrument (None = all)
         self._conv = {}  # int64 buffers for labels / mask / lengths given in another integer dtype
-        self._order_ws = None  # int32 [B*T]: a ragged batch's experience-row order (trlx_lsm_gather_fwd_ragged)
+        self._order_ws = None  # a ragged batch's row order (trlx_ragged_order_bytes; trlx_lsm_gather_fwd_ragged)
         self._ar_work = None  # pending whitening all-reduce (pipelined schedule)
         self._ar_group = None
         self._lp_bufs = None  # pipelined schedule: two (lp_old, ref_lp) pairs
@@ -326,11 +326,7 @@ class PPOHotPath:
         rows = (logits.data_ptr(), ref_logits.data_ptr(), _lib.dtype_code(logits), B, T, V, logits.stride(0),
                 logits.stride(1), labels.data_ptr(), labels.stride(0), labels.stride(1))
         outs = (self.lp_old[b0].data_ptr(), self.ref_lp[b0].data_ptr(), _lib.F32)
-        order = None
-        if lengths is not None:  # scratch for the valid-rows-first dispatch order
-            if self._order_ws is None:
-                self._order_ws = torch.empty(self.B * T, dtype=torch.int32, device=self.device)
-            order = self._order_ws.data_ptr()
+        order = self._order_scratch() if lengths is not None else None
         if timed:
             self._ev("experience", s)
         if self._tail_pending is not None:  # the previous step's loss tail rides this launch
@@ -343,6 +339,13 @@ class PPOHotPath:
             _lib.call("trlx_lsm_gather_fwd", *rows, *outs, None, None, s.cuda_stream)
         if timed:
             self._ev_end("experience", s)
+
+    def _order_scratch(self):
+        """Device scratch of a ragged batch's row order (trlx_ragged_order_bytes)."""
+        if self._order_ws is None:
+            self._order_ws = torch.empty(_lib.query("trlx_ragged_order_bytes", self.B, self.T), dtype=torch.uint8,
+                                         device=self.device)
+        return self._order_ws.data_ptr()
 
     def _launch_pending_tail(self, s):
         """Run a deferred loss tail by itself (nothing to fold it into)."""
@@ -438,8 +441,13 @@ class PPOHotPath:
                 h = h.contiguous()
             if w.stride(1) != 1 or w.stride(0) % 8 or w.data_ptr() % 16:
                 w = w.contiguous()
-            _lib.call("trlx_lmhead_logprobs", h.data_ptr(), h.stride(1), w.data_ptr(), w.stride(0), N, H, V,
-                      labels.data_ptr(), 1, out.data_ptr(), _lib.F32, None, self.lm_ws.data_ptr(), s.cuda_stream)
+            if lengths is not None:  # ragged: the padding's tokens skip the GEMM tiles (lp = 0)
+                _lib.call("trlx_lmhead_logprobs_ragged", h.data_ptr(), h.stride(1), w.data_ptr(), w.stride(0), N, H,
+                          V, labels.data_ptr(), 1, lengths.data_ptr(), T, self._order_scratch(), out.data_ptr(),
+                          _lib.F32, None, self.lm_ws.data_ptr(), s.cuda_stream)
+            else:
+                _lib.call("trlx_lmhead_logprobs", h.data_ptr(), h.stride(1), w.data_ptr(), w.stride(0), N, H, V,
+                          labels.data_ptr(), 1, out.data_ptr(), _lib.F32, None, self.lm_ws.data_ptr(), s.cuda_stream)
         self._ev_end("experience", s)
         self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
         return self.lp_old, self.ref_lp
