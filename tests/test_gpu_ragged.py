@@ -261,3 +261,34 @@ def test_fused_abi_ragged_step():
     for i, k in enumerate(P.STATS_KEYS):
         assert st[i] == pytest.approx(float(ref["stats"][k]), rel=1e-5, abs=1e-6), k
     assert int(x["lengths"].sum()) < B * Tn  # a ragged batch
+
+
+@pytest.mark.parametrize("B,Tn,V", [(1100, 3, 4099), (2100, 2, 32128)])
+def test_ragged_order_many_rollouts(B, Tn, V):
+    """k_ragged_order over more rollouts than its workgroup has threads (chunked scan with a
+    carry): the list is valid-first in row order, the count follows, and the ordered launch
+    gives the natural-order launch's bits (lengths include 0 and values beyond T)."""
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, Tn, V, generator=g).to(torch.bfloat16).to(DEV)
+    y = torch.randint(0, V, (B, Tn), generator=g).to(DEV)
+    L = torch.randint(0, Tn + 2, (B,), generator=g)
+    Ld = L.to(DEV)
+    nb = _lib.query("trlx_ragged_order_bytes", B, Tn)
+    order = torch.zeros(nb // 4, dtype=torch.int32, device=DEV)
+    outs = []
+    for o in (None, order):
+        lp0, lp1 = torch.full((B, Tn), 7.0, device=DEV), torch.full((B, Tn), 7.0, device=DEV)
+        _lib.call("trlx_lsm_gather_fwd_ragged", x.data_ptr(), x.data_ptr(), _lib.BF16, B, Tn, V, x.stride(0),
+                  x.stride(1), y.data_ptr(), Tn, 1, Ld.data_ptr(), None if o is None else o.data_ptr(), lp0.data_ptr(),
+                  lp1.data_ptr(), _lib.F32, torch.cuda.current_stream().cuda_stream)
+        outs.append((lp0.cpu(), lp1.cpu()))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    if V == 32128:  # the resident rows (and so the order) were used
+        Lc = L.clamp(0, Tn)
+        want = [b * Tn + t for b in range(B) for t in range(int(Lc[b]))]
+        want += [~(b * Tn + t) for b in range(B) for t in range(int(Lc[b]), Tn)]
+        got = order.cpu().tolist()
+        assert got[:B * Tn] == want and got[B * Tn] == int(Lc.sum())
+    pad = torch.arange(Tn)[None, :] >= L[:, None]
+    assert torch.equal(outs[1][0][pad], torch.zeros(int(pad.sum())))
