@@ -23,7 +23,7 @@ def main():
     p.add_argument("--config", default="c3")
     p.add_argument("--steps", type=int, default=60)
     p.add_argument("--rounds", type=int, default=3)
-    p.add_argument("--orders", default="0", help="tuning ragged_order values to compare (0 b-major, 1 t-major)")
+    p.add_argument("--orders", default="0", help="tuning ragged_order values to compare (0 valid rows first, 1 natural order)")
     a = p.parse_args()
     import torch
     import torch.distributed as dist
