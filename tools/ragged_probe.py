@@ -23,7 +23,8 @@ def main():
     p.add_argument("--config", default="c3")
     p.add_argument("--steps", type=int, default=60)
     p.add_argument("--rounds", type=int, default=3)
-    p.add_argument("--orders", default="0", help="tuning ragged_order values to compare (0 valid rows first, 1 natural order)")
+    p.add_argument("--orders", default="0", help="tuning values to compare (ragged_order / loss_order: 0 valid rows first, 1 natural order)")
+    p.add_argument("--key", default="ragged_order", help="the tuning key --orders sets (ragged_order or loss_order)")
     a = p.parse_args()
     import torch
     import torch.distributed as dist
@@ -60,13 +61,13 @@ def main():
         for name, o in runs:
             key = f"{name} o{o}" if len(orders) > 1 else name
             x["lengths"], x["mask"] = pats[name]
-            _lib.set_tuning("ragged_order", o)
+            _lib.set_tuning(a.key, o)
             bench.settle_and_warm(step, torch, ns, dev)
             el, km, _ = bench.timed_run(step, hp, torch, dist, ns, dev, 1, {"experience", "loss"})
             res[key].append((el / a.steps * 1e3, km["experience"] * 1e3, km["loss"] * 1e3))
             print(f"round {rnd} {key:12s} step {res[key][-1][0]:.4f} ms  E {res[key][-1][1]:7.2f} us  "
                   f"L {res[key][-1][2]:7.2f} us", flush=True)
-    _lib.set_tuning("ragged_order", 0)
+    _lib.set_tuning(a.key, 0)
     fill = float(L.sum()) / (B * T)
     print(f"{a.config} {B}x{T}x{V}: random fill {fill:.4f}")
     for name, r in res.items():
