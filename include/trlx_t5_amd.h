@@ -97,7 +97,7 @@ int trlx_lsm_gather_fwd(const void* x0, const void* x1, int dtype,
  * t >= lengths[b] is store padding — ppo_pipeline.py:47-65 pads each element's logprobs with
  * 0.0 — so its lp is 0 and the row is NOT read (the bytes of a batch of decoder lengths L_b
  * are those of its sum(L_b) tokens).  lengths == NULL: trlx_lsm_gather_fwd.  order_ws (or
- * NULL): trlx_ragged_order_bytes(B, T) bytes of device scratch — a one-workgroup launch
+ * NULL): trlx_ragged_order_bytes(B, T) bytes of device scratch — a small launch
  * first orders the rows valid-first so the skipped rows do not interleave with them (the
  * scratch then holds the B·T row ids, valid first and ~id for the padding, and the count). */
 int64_t trlx_ragged_order_bytes(int64_t B, int64_t T);

@@ -27,6 +27,7 @@ for st in $steps; do
         c5) run ${TAG}_bench_c5 300 $B --config c5 --steps 100 --warmup 5 ;;
         strong) run ${TAG}_bench_c4_strong1024 300 $B --config c4 --global-batch 1024 --steps 50 --warmup 5 ;;
         prof) run ${TAG}_prof_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c2 -o run -- $B --steps 200 --warmup 5 ;;
+        prof_c3) run ${TAG}_prof_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c3 -o run -- $B --config c3 --steps 200 --warmup 5 ;;
         prof_c4) run ${TAG}_prof_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c4 -o run -- $B --config c4 --steps 200 --warmup 5 ;;
         prof_c5) run ${TAG}_prof_c5 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_c5 -o run -- $B --config c5 --steps 100 --warmup 5 ;;
         pmc)

@@ -263,11 +263,13 @@ def test_fused_abi_ragged_step():
     assert int(x["lengths"].sum()) < B * Tn  # a ragged batch
 
 
-@pytest.mark.parametrize("B,Tn,V", [(1100, 3, 4099), (2100, 2, 32128)])
+@pytest.mark.parametrize("B,Tn,V", [(1100, 3, 4099), (2100, 2, 32128), (1500, 1, 32128), (3, 700, 32128),
+                                    (37, 61, 32128)])
 def test_ragged_order_many_rollouts(B, Tn, V):
-    """k_ragged_order over more rollouts than its workgroup has threads (chunked scan with a
-    carry): the list is valid-first in row order, the count follows, and the ordered launch
-    gives the natural-order launch's bits (lengths include 0 and values beyond T)."""
+    """k_ragged_order over several workgroups of rows (rollouts straddling them, one row per
+    rollout, rollouts longer than a workgroup's rows): the list is valid-first in row order,
+    the count follows, and the ordered launch gives the natural-order launch's bits (lengths
+    include 0 and values beyond T)."""
     g = torch.Generator().manual_seed(B)
     x = torch.randn(B, Tn, V, generator=g).to(torch.bfloat16).to(DEV)
     y = torch.randint(0, V, (B, Tn), generator=g).to(DEV)

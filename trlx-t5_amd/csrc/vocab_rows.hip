@@ -246,53 +246,75 @@ __device__ __forceinline__ bool pad_row(const RowArgs& a, int64_t row) {
 // order, then the padding rows as ~row.  Measured (tools/ragged_probe.py): the same skipped
 // rows cost ~20 us more at C3 when they are interleaved with the valid rows in dispatch order
 // than when they come after them (a skipped workgroup's short life idles its slot), so the
-// launch that takes its rows in this order pays this one-workgroup launch instead.
-// One workgroup; rollouts in chunks of kOrderThreads (B·T < 2^31).
-constexpr int kOrderThreads = 1024;
+// launch that takes its rows in this order pays this small launch instead (7.0 us with one
+// workgroup, round 3's first form, profiles/r03i_c3_kernel_stats.txt).
+// A grid of workgroups, each writing kOrderPos consecutive rows' entries (coalesced): every
+// workgroup sums the clamped lengths itself (all of them, and those before its first rollout),
+// scans its own rollouts' lengths in LDS, then places its rows — no pass over the batch by one
+// workgroup, no per-thread run of T scattered stores (B·T < 2^31).
+constexpr int kOrderThreads = 256;
+constexpr int kOrderPos = 1024;  // rows per workgroup: at most kOrderPos + 1 rollouts
+__device__ inline int order_wave_sum(int v) {
+    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
 __global__ __launch_bounds__(kOrderThreads) void k_ragged_order(const int64_t* lengths, int B, int T, int* order,
                                                                 int* count) {
-    __shared__ int sh[kOrderThreads];
-    __shared__ int s_carry;
-    const int tid = threadIdx.x;
-    // pass 1: the number of valid rows
-    int mine = 0;
-    for (int b = tid; b < B; b += kOrderThreads) mine += int(min(max(lengths[b], int64_t(0)), int64_t(T)));
-    sh[tid] = mine;
+    __shared__ int s_len[kOrderPos + 1], s_vo[kOrderPos + 1];
+    __shared__ int s_red[2][kOrderThreads / kWave], s_wsum[kOrderThreads / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const int64_t n = int64_t(B) * T;
+    const int64_t p0 = int64_t(blockIdx.x) * kOrderPos, p1 = min(p0 + kOrderPos, n);
+    const int b0 = int(p0 / T), b1 = int((p1 - 1) / T) + 1, nb = b1 - b0;
+    // the valid rows in all, and before rollout b0; this workgroup's rollouts' lengths to LDS
+    int tot = 0, pre = 0;
+    for (int b = tid; b < B; b += kOrderThreads) {
+        const int Lb = int(min(max(lengths[b], int64_t(0)), int64_t(T)));
+        tot += Lb;
+        pre += b < b0 ? Lb : 0;
+        if (b >= b0 && b < b1) s_len[b - b0] = Lb;
+    }
+    tot = order_wave_sum(tot);
+    pre = order_wave_sum(pre);
+    if (lane == 0) {
+        s_red[0][w] = tot;
+        s_red[1][w] = pre;
+    }
     __syncthreads();
-    for (int s = kOrderThreads / 2; s > 0; s >>= 1) {
-        if (tid < s) sh[tid] += sh[tid + s];
-        __syncthreads();
+    int nvalid = 0, run = 0;
+    for (int k = 0; k < kOrderThreads / kWave; ++k) {
+        nvalid += s_red[0][k];
+        run += s_red[1][k];
     }
-    const int nvalid = sh[0];
-    if (tid == 0) {
-        s_carry = 0;
-        *count = nvalid;  // after the list (order scratch: trlx_ragged_order_bytes)
+    // exclusive scan of s_len: thread tid takes rollouts [tid·per, tid·per + per)
+    const int per = (nb + kOrderThreads - 1) / kOrderThreads;
+    const int i0 = min(nb, tid * per), i1 = min(nb, i0 + per);
+    int loc = 0;
+    for (int i = i0; i < i1; ++i) loc += s_len[i];
+    int inc = loc;
+    for (int off = 1; off < kWave; off <<= 1) {
+        const int u = __shfl_up(inc, off);
+        inc += lane >= off ? u : 0;
+    }
+    if (lane == kWave - 1) s_wsum[w] = inc;
+    __syncthreads();
+    for (int k = 0; k < w; ++k) run += s_wsum[k];
+    run += inc - loc;
+    for (int i = i0; i < i1; ++i) {
+        s_vo[i] = run;  // valid rows before rollout b0 + i
+        run += s_len[i];
     }
     __syncthreads();
-    // pass 2: exclusive scan of the clamped lengths per chunk; rollout b's valid rows go to
-    // [vo, vo + L_b), its padding rows to nvalid + (b·T − vo) onwards
-    for (int b0 = 0; b0 < B; b0 += kOrderThreads) {
-        const int b = b0 + tid;
-        const int Lb = b < B ? int(min(max(lengths[b], int64_t(0)), int64_t(T))) : 0;
-        sh[tid] = Lb;
-        __syncthreads();
-        for (int off = 1; off < kOrderThreads; off <<= 1) {  // inclusive Hillis-Steele scan
-            const int v = tid >= off ? sh[tid - off] : 0;
-            __syncthreads();
-            sh[tid] += v;
-            __syncthreads();
-        }
-        const int vo = s_carry + sh[tid] - Lb;
-        if (b < B) {
-            const int base = b * T;
-            for (int j = 0; j < Lb; ++j) order[vo + j] = base + j;
-            const int po = nvalid + (base - vo);
-            for (int j = Lb; j < T; ++j) order[po + (j - Lb)] = ~(base + j);
-        }
-        __syncthreads();
-        if (tid == kOrderThreads - 1) s_carry += sh[tid];
-        __syncthreads();
+    // row p = b·T + j: valid -> vo_b + j; padding -> after every valid row, in row order
+    for (int64_t p = p0 + tid; p < p1; p += kOrderThreads) {
+        const int b = int(p / T), j = int(p - int64_t(b) * T);
+        const int Lb = s_len[b - b0], vo = s_vo[b - b0];
+        if (j < Lb)
+            order[vo + j] = int(p);
+        else
+            order[nvalid + (int(p) - j - vo) + (j - Lb)] = ~int(p);
     }
+    if (blockIdx.x == 0 && tid == 0) *count = nvalid;  // after the list (trlx_ragged_order_bytes)
 }
 
 // Whether the mask can hold a zero: its sum (the launch's Σmask, one L2-resident scalar) short
@@ -1051,8 +1073,9 @@ static size_t carve_workspace(void* base, int64_t B, int64_t T, Workspace* w) {
 }
 
 int launch_ragged_order(const int64_t* lengths, int64_t B, int64_t T, int* order, hipStream_t stream) {
-    hipLaunchKernelGGL(k_ragged_order, dim3(1), dim3(kOrderThreads), 0, stream, lengths, int(B), int(T), order,
-                       order + B * T);
+    if (B * T == 0) return TRLX_OK;
+    hipLaunchKernelGGL(k_ragged_order, dim3(unsigned((B * T + kOrderPos - 1) / kOrderPos)), dim3(kOrderThreads), 0,
+                       stream, lengths, int(B), int(T), order, order + B * T);
     return check_launch("k_ragged_order");
 }
 
