@@ -6,8 +6,11 @@ import sys
 
 
 def short(name):
+    if "k_vocab_rows<" in name:  # <DT, NV, MODE, ...>: MODE 0 the experience (forward) rows, 2 the loss rows
+        mode = name.split("k_vocab_rows<", 1)[1].split(",")[2].strip()
+        return {"0": "E rows", "2": "L rows"}.get(mode, "rows(other)")
     for key, lab in (("k_vocab_rows<trlx::BF16T, 13, 0", "E rows"), ("k_vocab_rows<trlx::BF16T, 9, 2", "L rows"),
-                     ("k_vocab_rows", "rows(other)"), ("k_rollout_gae", "GAE tail"), ("k_rollout_loss", "loss tail"),
+                     ("k_vocab_rows", "rows(other)"), ("k_rollout_gae", "GAE tail"), ("k_ragged_order", "ragged order"), ("k_rollout_loss", "loss tail"),
                      ("k_ilql_rows", "ILQL rows"), ("k_ilql_prep", "ILQL prep"), ("k_ilql_finalize", "ILQL finalize"),
                      ("k_score_moments", "score moments"), ("k_whiten_coef", "whiten coef"), ("nccl", "RCCL (side)")):
         if key in name:
