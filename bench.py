@@ -34,6 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level table
 TIMER_EVERY = 4        # instrument one step in four: HIP events around the vocab-row launches (>= 5 samples
                        # in a 20-step run; a fully instrumented C2 step costs ~1.7 %, so one in four ~0.4 %)
 SETTLE_MAX_STEPS = 5000
+C3_GLOBAL_BATCH = 512  # BASELINE.json configs[2]: "batch 512, DP over 2/4 GPUs"
 
 CONFIGS = {
     # name: (rows per GPU, response tokens, vocab, description)      BASELINE.json configs[]
@@ -108,6 +109,10 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher rehearsal without a GPU: every rank joins a gloo group, checks its rank / world "
                         "against the others and rank 0 prints one JSON line (tests/test_host_cpu.py)")
+    p.add_argument("--rank-timeout", type=float, default=600.0,
+                   help="--gpus N launcher deadline in seconds: ranks still running then are stopped (SIGTERM, "
+                        "then SIGKILL), named on stderr, and the launcher exits 124 (0 = no deadline)")
+    p.add_argument("--dry-run-hang-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher test: a stuck rank
     return p.parse_args()
 
 
@@ -118,13 +123,38 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n, argv):
+RANK_KILL_GRACE_S = 10.0  # after SIGTERM, how long a rank gets before SIGKILL
+RC_RANK_TIMEOUT = 124     # launcher exit code when the deadline fired (as timeout(1))
+
+
+def _stop_ranks(procs, live, why):
+    """SIGTERM every live rank, SIGKILL the ones still alive after the grace period; by PID
+    (never by pattern).  Returns the ranks that had to be killed."""
+    import signal
+    for q in live:
+        q.send_signal(signal.SIGTERM)
+    t_end = time.monotonic() + RANK_KILL_GRACE_S
+    while any(q.poll() is None for q in live) and time.monotonic() < t_end:
+        time.sleep(0.05)
+    killed = [procs.index(q) for q in live if q.poll() is None]
+    for q in live:
+        if q.poll() is None:
+            q.send_signal(signal.SIGKILL)
+    if killed:
+        print(f"bench.py launcher: ranks {killed} ignored SIGTERM ({why}); killed", file=sys.stderr)
+    return killed
+
+
+def launch_ranks(n, argv, timeout_s=600.0):
     """`bench.py --gpus N` without an external launcher: start N child processes of this
     script (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1) and
     return the first non-zero exit code.  Runs BEFORE anything in this process touches the
     GPU (torch is not even imported) and never execs: the parent only waits.  Rank 0's
-    stdout carries the JSON line; if a rank fails, the others are terminated by PID."""
-    import signal
+    stdout carries the JSON line; if a rank fails, the others are terminated by PID.
+    Deadline (--rank-timeout): a rank that neither finishes nor fails — e.g. one blocked in
+    ncclCommInitRank after a peer died — would otherwise hold the parent until the driver's
+    own limit; when `timeout_s` expires every live rank gets SIGTERM, then SIGKILL, the
+    ranks that had not exited are named on stderr and the launcher returns 124."""
     import subprocess
     port = os.environ.get("MASTER_PORT") or str(_free_port())
     procs = []
@@ -134,6 +164,7 @@ def launch_ranks(n, argv):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
     rc = 0
     live = list(procs)
+    deadline = time.monotonic() + timeout_s if timeout_s and timeout_s > 0 else None
     while live:
         for p in list(live):
             code = p.poll()
@@ -144,12 +175,36 @@ def launch_ranks(n, argv):
                 rc = code if code > 0 else 128 - code
                 print(f"bench.py launcher: rank {procs.index(p)} exited with {code}; stopping the others",
                       file=sys.stderr)
-                for q in live:
-                    q.send_signal(signal.SIGTERM)
+                _stop_ranks(procs, live, f"rank {procs.index(p)} failed")
+        if live and deadline is not None and time.monotonic() >= deadline:
+            stuck = [procs.index(q) for q in live]
+            print(f"bench.py launcher: --rank-timeout {timeout_s:g} s expired; ranks {stuck} had not exited; "
+                  f"stopping them", file=sys.stderr)
+            _stop_ranks(procs, live, "deadline")
+            rc = rc or RC_RANK_TIMEOUT
+            break
         time.sleep(0.05)
     for p in procs:
         p.wait()
     return rc
+
+
+def resolve_shape(args, world):
+    """(rows per GPU, T, V, workload description) of this run; sets args.global_batch when
+    the config fixes the global batch.  C3 at N > 1 defaults to BASELINE.json's global batch of
+    512 (T5-base, "batch 512, DP over 2/4 GPUs": strong scaling, 256 / 128 rows per GPU); at
+    N = 1 it runs one 256-rollout DP2 shard.  Every other config defaults to its rows per GPU
+    (weak scaling) unless --global-batch is given."""
+    B, T, V, desc = CONFIGS[args.config]
+    if args.config == "c3" and world > 1 and not args.global_batch:
+        args.global_batch = C3_GLOBAL_BATCH
+        desc = f"{desc} (BASELINE C3 global batch {C3_GLOBAL_BATCH})"
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
+        B = args.global_batch // world
+        desc = f"{desc}; strong scaling: {args.global_batch} rollouts global, {B} per GPU"
+    return B, T, V, desc
 
 
 def dry_run(args):
@@ -160,16 +215,32 @@ def dry_run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if rank == args.dry_run_hang_rank:  # a rank that never finishes (and ignores SIGTERM)
+        import signal
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)
+        while True:
+            time.sleep(1)
+    B, T, V, desc = resolve_shape(args, world)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))  # a stand-in for the timed region: per-rank clocks differ
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         got = [None] * world
-        dist.all_gather_object(got, (rank, local))
+        dist.all_gather_object(got, (rank, local, elapsed))
         dist.destroy_process_group()
     else:
-        got = [(rank, local)]
+        got = [(rank, local, elapsed)]
     if rank == 0:
+        per_rank = [g[2] for g in sorted(got)]
+        got = [g[:2] for g in got]
         ok = sorted(got) == [(r, r) for r in range(world)]
-        print(json.dumps({"dry_run": True, "n_gpus": world, "requested": args.gpus, "ranks": got, "ok": ok}),
+        print(json.dumps({"dry_run": True, "n_gpus": world, "requested": args.gpus, "ranks": got, "ok": ok,
+                          "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world,
+                                     "scaling": "strong" if args.global_batch else "weak",
+                                     "comm_nranks": world},
+                          "rank_ms_per_step": {"min": round(min(per_rank) * 1e3, 4),
+                                               "max": round(max(per_rank) * 1e3, 4), "ranks": len(per_rank)}}),
               flush=True)
         if not ok:
             raise SystemExit(3)
@@ -395,15 +466,18 @@ def timed_run(step, hp, torch, dist, args, dev, world, names):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, dist.ReduceOp.MAX)
-        elapsed = float(t)
+    per_rank = [elapsed]
+    if world > 1:  # every rank's own clock (the spread says whether one rank held the others)
+        t = torch.zeros(world, dtype=torch.float64, device=dev)
+        t[dist.get_rank()] = elapsed
+        dist.all_reduce(t, dist.ReduceOp.SUM)
+        per_rank = t.tolist()
+        elapsed = max(per_rank)
     kern_ms, samples = {}, {}
     for name, evs in timers.items():  # HIP events on the launch stream, timed region only
         kern_ms[name] = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
         samples[name] = len(evs)
-    return elapsed, kern_ms, samples
+    return elapsed, kern_ms, samples, per_rank
 
 
 def pmc_traffic(key, dom):
@@ -459,7 +533,7 @@ def ppo_setup(torch, P, args, B, T, V, dev, rank, masked, ldt, world=1, comm=Non
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout))
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: refusing a mislabelled run")
     if args.dry_run:
@@ -497,12 +571,7 @@ def main():
                 raise
             print(f"warning: RCCL helper unavailable ({e}); using torch.distributed collectives", file=sys.stderr)
 
-    B, T, V, desc = CONFIGS[args.config]
-    if args.global_batch:
-        if args.global_batch % world:
-            raise SystemExit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
-        B = args.global_batch // world
-        desc = f"{desc}; strong scaling: {args.global_batch} rollouts global, {B} per GPU"
+    B, T, V, desc = resolve_shape(args, world)
     if args.logits_dtype == "fp32" and args.config != "c5":
         desc = desc.replace("bf16 logits", "fp32 logits") + ("" if "logits" in desc else ", fp32 logits")
     ilql = args.config == "c5"
@@ -534,7 +603,7 @@ def main():
         traffic_key = None if args.global_batch else args.config + ("_fp32" if args.logits_dtype == "fp32" else "")
 
     warm_steps, warm_ms = settle_and_warm(step, torch, args, dev, world, dist)
-    elapsed, kern_ms, samples = timed_run(step, hp, torch, dist, args, dev, world, names)
+    elapsed, kern_ms, samples, per_rank = timed_run(step, hp, torch, dist, args, dev, world, names)
     roof = roofline(kern_ms, samples, ab, tokens, doms, elapsed, args.steps, traffic_key)
 
     # Secondary line (C2 at N=1): the same step with fp32 logits (the reference's GPT path,
@@ -546,7 +615,7 @@ def main():
         torch.cuda.empty_cache()
         hp32, step32, x32 = ppo_setup(torch, P, args, B, T, V, dev, rank, masked, torch.float32, world, comm)
         w32, wms32 = settle_and_warm(step32, torch, args, dev)
-        el32, km32, sm32 = timed_run(step32, hp32, torch, dist, args, dev, world, names)
+        el32, km32, sm32, _ = timed_run(step32, hp32, torch, dist, args, dev, world, names)
         fp32_line = {"value": round(tokens * args.steps / el32, 1), "unit": "tokens/s",
                      "ms_per_step": round(el32 / args.steps * 1e3, 4), "warmup_steps_run": w32,
                      "warmup_ms": round(wms32, 1),
@@ -586,7 +655,10 @@ def main():
             "data": "synthetic",
             "config": {"workload": desc, "rows_per_gpu": B, "global_batch": B * world, "seq_len": T, "vocab": V,
                        "logits_dtype": "fp32" if ilql else args.logits_dtype, "tokens_per_gpu_step": tokens,
-                       "parallelism": f"dp{world}", "schedule": schedule, "comm": comm_kind},
+                       "parallelism": f"dp{world}", "schedule": schedule, "comm": comm_kind,
+                       "comm_nranks": comm.nranks if comm is not None else (world if use_dist else None)},
+            "rank_ms_per_step": {"min": round(min(per_rank) / args.steps * 1e3, 4),
+                                 "max": round(max(per_rank) / args.steps * 1e3, 4), "ranks": len(per_rank)},
             **({"ragged": {"valid_token_fraction": round(fill, 4),
                            "note": "tokens counts every decoder position of the padded batch; logits rows past a "
                                    "rollout's length are store padding (lp = 0) and masked loss rows have zero "

@@ -29,7 +29,7 @@ def whiten_stats_worker(rank, world, port, xs, q):
     dist.destroy_process_group()
 
 
-def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank", mode="step"):
+def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank", mode="step", cfg_kwargs=None):
     """One rank of a DP PPO step on cuda:0 over gloo (the product's exchange: the whitening
     record all-reduce inside PPOHotPath.experience).  Rank r takes the contiguous row block
     r of the batch (accelerate_ppo_model.py:146-148 sharding)."""
@@ -40,7 +40,8 @@ def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank", mode="s
     dev = torch.device("cuda:0")
     sh = {k: (v.chunk(world, dim=0)[rank].contiguous().to(dev) if v is not None else None) for k, v in inputs.items()}
     B, T, V = sh["logits"].shape
-    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05, loss_norm=loss_norm)
+    hp = P.PPOHotPath(P.PPOConfig(**(cfg_kwargs or {})), B, T, V, torch.bfloat16, dev, kl_coef=0.05,
+                      loss_norm=loss_norm)
     args = (sh["logits"], sh["ref_logits"], sh["new_logits"], sh["labels"], sh["old_values"], sh["values"],
             sh["scores"])
     if mode == "pipelined":  # split-beta schedule: one batch through pipeline_step + flush
@@ -52,7 +53,7 @@ def hot_path_step_worker(rank, world, port, inputs, q, loss_norm="rank", mode="s
     torch.cuda.synchronize()
     q.put((rank, {"lp": hp.lp_old.cpu(), "rewards": hp.rewards.cpu(), "adv_stats": hp.adv_stats.cpu(),
                   "loss": loss.cpu(), "dlogits": dlogits.float().cpu(), "dvalues": dvalues.cpu(),
-                  "stats": stats.cpu(), "returns": hp.returns.cpu()}))
+                  "stats": stats.cpu(), "returns": hp.returns.cpu(), "adv_raw": hp.adv_raw.cpu()}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -221,6 +222,51 @@ def rccl_world1_worker(port, inputs, xs_all, q):
         surf[key] = (float(mean), float(var), float(count), P.whiten(xd).float().cpu().numpy(),
                      P.whiten(xd, shift_mean=False).float().cpu().numpy())
     res["surface"] = surf
+    q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def rccl_scores_reuse_worker(port, inputs, q):
+    """under the lag schedule the side stream's moments kernel reads the
+    caller's `scores` after pipeline_step returns.  Each batch's scores are a fresh tensor
+    dropped right after the call, and a same-sized tensor allocated at once and filled with
+    NaN on the main stream (the caching allocator hands it the freed block unless the side
+    stream's use was recorded).  The controller state must equal the serial schedule's."""
+    import torch.distributed as dist
+    import trlx_t5_amd as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    comm = P.RcclComm.from_process_group(device=dev)
+    res = {}
+    for mode in ("serial", "pipelined"):
+        cfg = P.PPOConfig(scale_reward=False)  # lag: the moments ride the side stream
+        B, T, V = inputs[0]["logits"].shape
+        ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B)
+        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, comm=comm, split_beta=True,
+                          defer_tail=True)
+        fixed = [{k: v.to(dev) for k, v in b.items() if k != "scores"} for b in inputs]
+        poison = []
+        for b, xb in zip(inputs, fixed):
+            sc = b["scores"].to(dev)  # a fresh allocation per batch
+            args = (xb["logits"], xb["ref_logits"], xb["new_logits"], xb["labels"], xb["old_values"], xb["values"], sc)
+            if mode == "pipelined":
+                hp.pipeline_step(*args)
+                assert hp._lag, "the test needs the lag schedule"
+            else:
+                hp.step(*args)
+            del sc, args
+            p = torch.empty(B, dtype=torch.float32, device=dev)  # the freed block, if nothing held it
+            p.fill_(float("nan"))
+            poison.append(p)
+        if mode == "pipelined":
+            hp.pipeline_flush()
+        hp.wait_stats()
+        torch.cuda.synchronize()
+        res[mode] = ctl.state.cpu().numpy()
+    comm.close()
     q.put(res)
     dist.barrier()
     dist.destroy_process_group()

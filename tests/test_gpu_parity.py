@@ -230,12 +230,43 @@ def test_moments_and_global_statistics_single_process():
 def test_running_moments_kat_device(golden):
     z = golden("host_state")
     rm = P.RunningMoments()
+    assert (rm.mean, rm.var, rm.std, rm.count) == (0, 1, 1, 1e-24)  # modeling.py:78-81
+    n = 0
     for i in range(4):
         a = T(z[f"rm/{i}/in"]).float()
         bm, bs = rm.update(cuda(a))
+        n += a.numel()
+        # the reference's types (modeling.py:83-104): xs-dtype 0-d tensors on xs's device
+        for t in (bm, bs, rm.mean, rm.var, rm.std):
+            assert isinstance(t, torch.Tensor) and t.dim() == 0 and t.dtype == a.dtype and t.device == DEV
+        assert isinstance(rm.count, float) and rm.count == pytest.approx(1e-24 + n)
         assert float(bm) == pytest.approx(float(z[f"rm/{i}/batch_mean"]), rel=1e-6, abs=1e-6)
         assert float(bs) == pytest.approx(float(z[f"rm/{i}/batch_std"]), rel=1e-6)
-        assert rm.std == pytest.approx(float(z[f"rm/{i}/std"]), rel=1e-6)
+        assert float(rm.std) == pytest.approx(float(z[f"rm/{i}/std"]), rel=1e-6)
+        assert float(rm.mean) == pytest.approx(float(z[f"rm/{i}/mean"]), rel=1e-6, abs=1e-6)
+    b16 = P.RunningMoments()
+    bm, bs = b16.update(cuda(T(z["rm/0/in"])).to(torch.bfloat16))
+    assert bm.dtype == bs.dtype == b16.std.dtype == torch.bfloat16
+
+
+def test_prepare_scores_one_launch_no_host_sync(golden):
+    """ppo_orchestrator.py:96-112 through trlx_score_ctl_update on the RunningMoments record:
+    the scaled / clipped scores and the batch moments against the oracle's ScoreControl."""
+    g = torch.Generator().manual_seed(11)
+    for mode in (False, "running", "ref"):
+        rm = P.RunningMoments()
+        osc = orc.ScoreControl(mode, 1.5)
+        ref_std = None
+        for k in range(3):
+            sc = torch.rand(24, generator=g) * 8 - 4
+            if mode == "ref" and ref_std is None:
+                ref_std = float(sc.std())
+                osc.ref_std = torch.tensor(ref_std)
+            out, bm, bs = P.prepare_scores(cuda(sc), rm, mode, 1.5, ref_std=ref_std)
+            want, wbm, wbs = osc(sc)
+            torch.testing.assert_close(out.cpu(), want, rtol=1e-6, atol=1e-6)
+            assert float(bm) == pytest.approx(float(wbm), rel=1e-6, abs=1e-6)
+            assert float(bs) == pytest.approx(float(wbs), rel=1e-6)
 
 
 # ------------------------------------------------------------------ A5 GAE

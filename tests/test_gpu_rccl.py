@@ -72,3 +72,22 @@ def test_rccl_world1_hot_path_and_drop_in_surface(golden):
         tol = dict(rtol=2 ** -7, atol=1e-2) if bf else dict(rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(torch.from_numpy(w), T(z[f"{k}/dist1/whiten"]).float(), **tol)
         torch.testing.assert_close(torch.from_numpy(w2), T(z[f"{k}/dist1/whiten_noshift"]).float(), **tol)
+
+
+def test_rccl_lag_schedule_scores_freed_after_call():
+    """The side-stream score moments of the lag schedule read the caller's scores after
+    pipeline_step has returned: dropping them (and reusing their memory on the main stream)
+    must not change the RunningMoments merge (scores.record_stream)."""
+    import torch.multiprocessing as mp
+    import dist_workers
+    batches = [_batch(6, 19, 1031, 90 + i) for i in range(4)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 90
+    p = ctx.Process(target=dist_workers.rccl_scores_reuse_worker, args=(port, batches, q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert np.all(np.isfinite(res["pipelined"]))
+    assert np.array_equal(res["serial"], res["pipelined"])

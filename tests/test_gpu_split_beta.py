@@ -184,3 +184,24 @@ def test_whiten_coef_matches_fold():
     assert coef[0].item() == pytest.approx(mu, rel=1e-5, abs=1e-6)
     assert coef[1].item() == pytest.approx((A.var(unbiased=True).item() + 1e-8) ** -0.5, rel=1e-5)
     assert coef[2].item() == np.float32(0.05)
+
+
+def test_serial_entry_points_refuse_a_pending_pipeline_batch():
+    """ADVICE r03: after pipeline_step the last batch's loss exists only inside the pipeline;
+    step() / experience() / experience_from_hidden() raise until pipeline_flush() ran it."""
+    B, Tn, V = 4, 9, 1031
+    x = _inputs(B, Tn, V, 4242)
+    hp = P.PPOHotPath(P.PPOConfig(), B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05, defer_tail=True)
+    assert hp.pipeline_step(*_args(x)) is None
+    a = _args(x)
+    with pytest.raises(RuntimeError, match="pipeline_flush"):
+        hp.step(*a)
+    with pytest.raises(RuntimeError, match="pipeline_flush"):
+        hp.experience(a[0], a[1], a[3], a[4], a[6])
+    h = torch.zeros(B, Tn, 64, dtype=torch.bfloat16, device=DEV)
+    w = torch.zeros(V, 64, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="pipeline_flush"):
+        hp.experience_from_hidden(h, w, h, w, a[3], a[4], a[6])
+    assert hp.pipeline_flush() is not None
+    hp.step(*a)  # fine again
+    torch.cuda.synchronize()

@@ -230,6 +230,45 @@ def test_bench_launcher_spawns_ranks(n):
     assert rec["n_gpus"] == n and rec["ok"] and sorted(map(tuple, rec["ranks"])) == [(i, i) for i in range(n)]
 
 
+def _bench_env():
+    return {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+
+
+def test_bench_launcher_reports_rank_fields():
+    """The line carries the communicator's rank count and the per-rank step-time spread;
+    C3 at N > 1 defaults to BASELINE's global batch 512 (strong scaling)."""
+    import json
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--config", "c3", "--dry-run"],
+                       capture_output=True, text=True, env=_bench_env(), timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["config"]["global_batch"] == 512 and rec["config"]["rows_per_gpu"] == 128
+    assert rec["config"]["scaling"] == "strong" and rec["config"]["comm_nranks"] == 4
+    rs = rec["rank_ms_per_step"]
+    assert rs["ranks"] == 4 and 0 < rs["min"] < rs["max"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c2", "--dry-run"],
+                       capture_output=True, text=True, env=_bench_env(), timeout=240)
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["config"]["global_batch"] == 256 and rec["config"]["scaling"] == "weak"
+
+
+def test_bench_launcher_deadline_stops_a_stuck_rank():
+    """A rank that never exits (and ignores SIGTERM) no longer holds the launcher: after
+    --rank-timeout every live rank is stopped (SIGTERM, then SIGKILL), the stuck ranks are
+    named on stderr and the launcher exits non-zero."""
+    import sys
+    import time
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--dry-run-hang-rank", "1", "--rank-timeout", "8"],
+                       capture_output=True, text=True, env=_bench_env(), timeout=120)
+    took = time.monotonic() - t0
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    assert "had not exited" in r.stderr and "1]" in r.stderr and "killed" in r.stderr
+    assert took < 60
+
+
 def test_bench_refuses_mislabelled_world():
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([__import__("sys").executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dry-run"],

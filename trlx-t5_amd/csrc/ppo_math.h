@@ -41,12 +41,19 @@ __device__ __forceinline__ float ppo_policy_dlp(float lp, float olp, float A, fl
 // mean and rsqrt(var + 1e-8) from a {sum, sumsq, count} fp64 record (modeling.py:24-34):
 // var = M2/count in the distributed branch, M2/(count-1) for torch.var_mean.
 // No fp64 division (its v_div_scale/v_rcp sequence would set the fused row kernel's
-// register peak): mean is an fp32 division, and M2 = Σx² − 2·m·Σx + n·m² with m = the
-// fp32 mean is exact up to n·(μ − m)² (~1e-14 relative), evaluated with fp64 fmas.
+// register peak): 1/n is the fp32 reciprocal refined by two Newton steps in fp64 (exact to
+// ~1 ulp of a double), so mu = fl32(Σx · 1/n) is the correctly rounded mean (torch's fp32
+// mean of an fp64 accumulation) even at a large common offset, where rounding Σx to fp32
+// first could move mu by an ulp (1e-3 at |mu| ~ 1e4: every whitened value would shift by
+// it).  M2 = Σx² − 2·m·Σx + n·m² with m = the fp32 mean is exact up to n·(μ − m)² (~1e-14
+// relative), evaluated with fp64 fmas.
 __device__ __forceinline__ void whiten_coeffs(const double* st, int unbiased, float& mu, float& rstd) {
     const double sum = st[0], sumsq = st[1], cnt = st[2];
     const float nf = float(cnt);
-    mu = float(sum) / nf;
+    double r = double(__frcp_rn(nf));
+    r = r * fma(-cnt, r, 2.0);
+    r = r * fma(-cnt, r, 2.0);
+    mu = float(sum * r);
     const double m = double(mu);
     double m2 = fma(m * cnt, m, fma(-2.0 * m, sum, sumsq));
     if (m2 < 0) m2 = 0;

@@ -7,7 +7,7 @@ computation is a HIP kernel from libtrlx_t5_amd.so (no CPU path):
   whiten                 modeling.py:24-34  biased (distributed branch) / unbiased (var_mean)
   logprobs_from_logits   modeling.py:37-41  fused single-pass log-softmax + gather, autograd
   flatten_dict           modeling.py:44-57  host utility
-  RunningMoments         modeling.py:72-104 Chan merge of batch moments (host scalars)
+  RunningMoments         modeling.py:72-104 Chan merge of batch moments (device fp64 record)
 """
 from collections.abc import MutableMapping
 from typing import Tuple
@@ -188,27 +188,91 @@ def merge_moments(mean, var, count, xs_mean, xs_var, xs_count):
 
 
 class RunningMoments:
-    """Running mean / std of a scalar stream (modeling.py:72-104).
+    """Running mean / std of a scalar stream (modeling.py:72-104), device resident.
 
-    Batch moments come from the device moments kernel (all-reduced across ranks when
-    torch.distributed is initialised); the merge itself is host fp64 scalar arithmetic.
+    State: one fp64 controller record on the device of the first batch (TRLX_CTL_* slots,
+    the layout PPOControlState uses).  update(xs) = the device moments kernel {Σx, Σx², n}
+    (all-reduced across ranks when torch.distributed is initialised: get_global_statistics
+    semantics, biased variance; torch.var_mean(unbiased=False) otherwise) and the Chan merge
+    kernel (trlx_score_moments_merge, term for term modeling.py:91-102, in fp64) — no host
+    synchronisation.  Types follow the reference: update returns (batch mean, unbiased batch
+    std) as 0-d tensors of xs.dtype on xs.device; after the first update mean / var / std are
+    0-d device tensors (xs.dtype), and count is a Python float without a process group (the
+    reference's 1e-24 + numel) or a 0-d device tensor with one (its all-reduced count).
+    Before the first update they are the reference's initial Python numbers.
     """
 
     def __init__(self):
-        self.mean = 0.0
-        self.std = 1.0
-        self.var = 1.0
-        self.count = 1e-24
+        self._st = None       # fp64 [TRLX_CTL_SLOTS] device record, allocated by the first update
+        self._dtype = None    # dtype of the last batch (the reference's attribute tensors carry it)
+        self._count = 1e-24   # host count (non-distributed updates only)
+        self._host_count = True
+
+    def _slot(self, k, init):
+        if self._st is None:
+            return init
+        return self._st[k].to(self._dtype)
+
+    @property
+    def mean(self):
+        return self._slot(_lib.CTL_MEAN, 0)
+
+    @property
+    def var(self):
+        return self._slot(_lib.CTL_VAR, 1)
+
+    @property
+    def std(self):
+        return self._slot(_lib.CTL_STD, 1)
+
+    @property
+    def count(self):
+        if self._st is None or self._host_count:
+            return self._count
+        return self._st[_lib.CTL_COUNT].to(self._dtype)
 
     def update(self, xs: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        _lib.require_cuda(xs)
+        s = _lib.stream_of(xs)
+        if self._st is None:
+            self._st = torch.empty(_lib.CTL_SLOTS, dtype=torch.float64, device=xs.device)
+            _lib.call("trlx_ctl_init", _lib.ptr(self._st), 0.0, 0.0, float("nan"), 0, s)
+        elif self._st.device != xs.device:
+            raise ValueError(f"RunningMoments state lives on {self._st.device}, batch on {xs.device}")
         st = moments(xs)
-        if dist.is_available() and dist.is_initialized():
+        use_dist = dist.is_available() and dist.is_initialized()
+        if use_dist:
             _allreduce_moments(st)
-        s, ss, n = st[:3].tolist()
-        xs_mean = s / n
-        xs_var = max(ss - s * xs_mean, 0.0) / n  # biased, as var_mean(unbiased=False)
-        self.mean, self.var, self.std, self.count = merge_moments(
-            float(self.mean), float(self.var), float(self.count), xs_mean, xs_var, n)
-        batch_std = (xs_var * n / (n - 1)) ** 0.5 if n > 1 else float("nan")
-        return (torch.tensor(xs_mean, dtype=torch.float64),
-                torch.tensor(batch_std, dtype=torch.float64))
+            self._host_count = False
+        else:
+            self._count = self._count + xs.numel()
+        _lib.call("trlx_score_moments_merge", _lib.ptr(self._st), _lib.ptr(self._st), _lib.ptr(st), s)
+        self._dtype = xs.dtype
+        return (self._st[_lib.CTL_BATCH_MEAN].to(xs.dtype), self._st[_lib.CTL_BATCH_STD].to(xs.dtype))
+
+    def _update_scaled(self, scores: torch.Tensor, mode: int, clip: float, ref_std=None):
+        """update(scores) fused with the orchestrator's scale / clip (ppo.prepare_scores): one
+        trlx_score_ctl_update launch on this record (local two-pass fp64 batch moments, or the
+        all-reduced ones under a process group).  Returns (scores', batch mean, batch std)."""
+        _lib.require_cuda(scores)
+        x = scores.to(torch.float32).contiguous()
+        if x.numel() == 0:
+            raise ValueError("prepare_scores: empty score batch")
+        s = _lib.stream_of(x)
+        if self._st is None:
+            self._st = torch.empty(_lib.CTL_SLOTS, dtype=torch.float64, device=x.device)
+            _lib.call("trlx_ctl_init", _lib.ptr(self._st), 0.0, 0.0, float("nan"), 0, s)
+        g = None
+        if dist.is_available() and dist.is_initialized():
+            g = _allreduce_moments(moments(x))
+            self._host_count = False
+        else:
+            self._count = self._count + x.numel()
+        if mode == _lib.SCALE_REF:  # the caller's ref_std (ppo_orchestrator.py:96-98 keeps it host side)
+            self._st[_lib.CTL_REF_STD].fill_(float(ref_std))
+            self._st[_lib.CTL_REF_SET].fill_(1.0)
+        out = torch.empty_like(x)
+        c = _lib.ScoreCtl(_lib.ptr(self._st), _lib.ptr(self._st), _lib.ptr(g), mode, clip)
+        _lib.call("trlx_score_ctl_update", _lib.ptr(x), _lib.F32, x.numel(), c, _lib.ptr(out), _lib.F32, s)
+        self._dtype = x.dtype
+        return out.view_as(scores), self._st[_lib.CTL_BATCH_MEAN].to(x.dtype), self._st[_lib.CTL_BATCH_STD].to(x.dtype)

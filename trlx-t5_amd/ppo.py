@@ -71,19 +71,22 @@ def stats_dict(stats_dev: torch.Tensor) -> dict:
 # ------------------------------------------------------------------ A2
 def prepare_scores(scores: torch.Tensor, running: RunningMoments, scale_reward, cliprange_reward,
                    ref_std=None):
-    """Score scaling / clipping of ppo_orchestrator.py:96-112 (host control flow, device math).
+    """Score scaling / clipping of ppo_orchestrator.py:96-112 in ONE device launch
+    (trlx_score_ctl_update on the RunningMoments record: the batch moments, the Chan merge,
+    then clip(scores / scale, ±cliprange_reward)); no host synchronisation.
 
     Returns (scores, batch_mean, batch_std).  `ref_std` is the std of the first rollout's
     scores when scale_reward == "ref" (the caller keeps it, as the orchestrator does).
+    Under torch.distributed the batch moments are all-reduced first (RunningMoments.update's
+    get_global_statistics branch, modeling.py:85-86).
     """
-    batch_mean, batch_std = running.update(scores)
-    if scale_reward == "running":
-        scores = scores / float(running.std)
-    elif scale_reward == "ref":
-        scores = scores / ref_std
-    if cliprange_reward:
-        scores = torch.clip(scores, -cliprange_reward, cliprange_reward)
-    return scores, batch_mean, batch_std
+    mode = {False: _lib.SCALE_NONE, None: _lib.SCALE_NONE, "running": _lib.SCALE_RUNNING,
+            "ref": _lib.SCALE_REF}.get(scale_reward)
+    if mode is None:
+        raise ValueError(f"scale_reward must be False, 'running' or 'ref', got {scale_reward!r}")
+    if mode == _lib.SCALE_REF and ref_std is None:
+        raise ValueError("scale_reward='ref' needs ref_std (the first rollout's score std)")
+    return running._update_scaled(scores, mode, float(cliprange_reward or 0.0), ref_std)
 
 
 def kl_penalty_rewards(logprobs: torch.Tensor, ref_logprobs: torch.Tensor, kl_coef: float,

@@ -287,8 +287,18 @@ class PPOHotPath:
                 self._vec(scores, (B,), "scores", (torch.float32,)))
 
     # -------------------------------------------------------------- K1
+    def _no_pipeline_pending(self, what):
+        """The serial entry points after pipeline_step: its last batch's loss (and, under the lag
+        schedule, that batch's RunningMoments merge) exist only inside the pipeline until
+        pipeline_flush(); a serial call would silently drop them."""
+        if self._pending is not None or self._lag:
+            raise RuntimeError(f"{what}: pipeline_step has a pending batch (its loss"
+                               f"{' and score-moments merge' if self._lag else ''} not yet run): "
+                               f"call pipeline_flush() first")
+
     def experience(self, logits, ref_logits, labels, old_values, scores, lengths=None, mask=None, group=None):
         """K1 (+ all-reduce): lp, ref_lp, KL rewards, GAE, global whitening moments."""
+        self._no_pipeline_pending("experience")
         self._check(logits)
         self._check(ref_logits)
         if logits.stride() != ref_logits.stride():
@@ -392,6 +402,7 @@ class PPOHotPath:
         between the routes (tests/test_gpu_lmhead.py pins both against fp64 at realistic logit
         scale).  The gemm route keeps a [2, chunk, T, V] bf16 ring (LM_HEAD_CHUNK_TOKENS tokens per
         chunk: the full [2, B, T, V] logits never exist); release_lm_logits() frees it."""
+        self._no_pipeline_pending("experience_from_hidden")
         B, T, V = self.B, self.T, self.V
         for h, w in ((hidden, weight), (ref_hidden, ref_weight)):
             if h.dim() != 3 or tuple(h.shape[:2]) != (B, T) or w.dim() != 2 or w.shape[0] != V or \
@@ -523,6 +534,10 @@ class PPOHotPath:
                     if self._comm_stream is None:
                         self._comm_stream = torch.cuda.Stream(self.device)
                     done.wait(self._comm_stream)
+                    # the side stream reads the caller's scores: keep their memory from being
+                    # handed to a later allocation until that read has run (the caller
+                    # typically drops a batch's scores right after pipeline_step returns)
+                    scores.record_stream(self._comm_stream)
                     self._score_moments(scores, mom, self._comm_stream)
                     self._ar_work = self._side_allreduce([rec, mom[:3]], s, ready=done, issued=True)
             else:
@@ -684,7 +699,10 @@ class PPOHotPath:
         nothing else waits on the network.  Returns the PREVIOUS batch's (loss, stats,
         dlogits, dvalues) — valid until the next call; with defer_tail, loss / stats are final
         after wait_stats() — or None on the first call; pipeline_flush() runs the last pending
-        loss.  lp_old / ref_lp and the split buffers are double-buffered."""
+        loss.  lp_old / ref_lp and the split buffers are double-buffered.  Under a process group
+        without running-std score scaling (lag) the controller's RunningMoments run one batch
+        behind until pipeline_flush() merges the last batch's moments.  The serial entry points
+        (step / experience / experience_from_hidden) refuse to run while a batch is pending."""
         self._check(logits)
         self._check(ref_logits)
         if logits.stride() != ref_logits.stride():
