@@ -339,6 +339,45 @@ int trlx_lmhead_logprobs_ragged(const void* hidden, int64_t ldh, const void* wei
                                 int64_t T, void* order_ws, void* lp_out, int lp_dtype, float* lse_out,
                                 void* workspace, void* stream);
 
+/* ---------------------------------------------------------------- §8f rank 2, loss side: fused lm_head fwd + bwd
+ * The policy update's lm_head (ppo_models.py:640 T5, :274 GPT) + logprobs_from_logits
+ * (modeling.py:37-41) + autograd back through both (accelerate_ppo_model.py:96-118), with the
+ * [N, V] logits and dlogits never written: with p = softmax(h·Wᵀ) and g = d loss / d lp,
+ *   dh_t = g_t·(W[y_t] − Σ_v p_tv·W_v)      dW_v = Σ_t g_t·(1[y_t = v] − p_tv)·h_t.
+ * hidden [N, ldh] bf16 (N = B·T tokens, row t of rollout b = token b·T + t), weight [V, ldw]
+ * bf16 (nn.Linear layout), H in {512, 768}; dweight [V, lddw] of dw_dtype (overwritten); dhidden
+ * [N, lddh] of dh_dtype (bf16 / fp32, lddh a multiple of 4).  Three MFMA launches + small
+ * ones: a flash-style forward (online softmax and O = Σ_v P·W_v per token and vocab split), a
+ * per-token combine (lse, lp, g, dh) and a dW pass that recomputes each logits tile and
+ * accumulates dSᵀ·h; deterministic (fixed-order sums, no atomics).
+ * lm_workspace: trlx_lmhead_loss_workspace_bytes(N, H, V) bytes, no initialisation. */
+int64_t trlx_lmhead_loss_workspace_bytes(int64_t N, int64_t H, int64_t V);
+/* The PPO loss from the policy's last hidden states: trlx_ppo_loss_rows's arguments with the
+ * logits replaced by (hidden, weight) and dlogits by (dhidden, dweight) — same token records
+ * in `workspace` (trlx_ppo_rollout_loss then emits loss + stats), same whitening of adv_raw by
+ * `stats` (NULL: adv_raw used as given), dvalues, lp_out.  Tokens with mask == 0 are skipped
+ * (compacted out of all three MFMA passes: zero gradient, lp_out 0, their token records as
+ * the masked loss rows write them). */
+int trlx_ppo_loss_from_hidden(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B,
+                              int64_t T, int64_t H, int64_t V, const int64_t* labels, const void* old_lp,
+                              int old_dtype, const float* adv_raw, const double* stats, int unbiased,
+                              const int64_t* mask, const void* values, int v_dtype, const void* old_values,
+                              int ov_dtype, const void* returns, int r_dtype, float cliprange,
+                              float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
+                              int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues,
+                              void* workspace, void* lm_workspace, void* stream);
+/* The differentiable building block (logprobs_from_logits(lm_head(h), y) with autograd):
+ * forward -> lp [N] (lp_dtype), lse [N] fp32 and E = Σ_v p_tv·W_v [N, H] fp32 (saved for the
+ * backward); backward(grad = d loss / d lp [N], F32 / BF16) -> dhidden, dweight. */
+int trlx_lmhead_logprobs_fwd_saved(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
+                                   int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
+                                   int lp_dtype, float* lse_out, float* e_out, void* lm_workspace, void* stream);
+int trlx_lmhead_logprobs_bwd(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
+                             int64_t H, int64_t V, const int64_t* labels, int64_t lb, const void* grad,
+                             int grad_dtype, const float* lse, const float* e, void* dhidden, int64_t lddh,
+                             int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, void* lm_workspace,
+                             void* stream);
+
 /* ---------------------------------------------------------------- §8f rank 3: ILQL sampling step
  * One decode step of CausalLMWithValueHeads.generate (ilql_models.py:296-316) per row b:
  *   score = log_softmax(logits[b]) + beta*(min(tq0[b], tq1[b]) - vs[b])  (logits -inf where

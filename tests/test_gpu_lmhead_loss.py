@@ -1,0 +1,205 @@
+"""§8f-2, loss side: the fused lm_head forward + backward (csrc/lmhead_loss.hip).
+
+The reference's policy update runs lm_head -> [B, T, V] logits -> logprobs_from_logits -> PPO
+loss -> autograd back through both (accelerate_ppo_model.py:96-118, ppo_models.py:640 / :274,
+modeling.py:37-41, ppo_models.py:141-199).  The product computes lp, dh and dW from the hidden
+states without the logits / dlogits ever in HBM.  Checked here against the oracle's own ops
+(oracle.ppo_oracle, run with torch on the same device in fp32 — a floating-point kernel's
+reference) on the same bf16 hidden states / weights:
+  * lp, lse: fp32 MFMA accumulation vs the fp32 logits: rtol 1e-5-level (stated per test);
+  * dh, dW: the products use bf16 operands (P and dS tiles rounded to bf16, like the
+    reference's bf16 dlogits on the T5 path), so they are compared against the fp64 gradients
+    with the reference's OWN bf16 pipeline as the yardstick: the product's relative error
+    (Frobenius) must be within 2x the bf16 reference path's (bf16 logits, bf16 log-softmax
+    backward, bf16 GEMMs) and below 1e-2;
+  * the PPO loss, the 13 stats and dvalues at rtol 1e-4 / the loss rows' tolerances.
+Masked tokens are compacted out (their hidden rows are NaN-poisoned here and never read), the
+forward's fixed-offset softmax restarts when a later vocab tile's logits exceed the first
+tile's by more than e^60 (a case built for it), and two runs are bit-identical.
+"""
+import pytest
+import torch
+
+import trlx_t5_amd as P
+from oracle import ppo_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _operands(N, H, V, seed, wscale=0.05, hscale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    h = (torch.randn(N, H, generator=g) * hscale).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * wscale).to(torch.bfloat16)
+    y = torch.randint(0, V, (N,), generator=g)
+    return h, w, y
+
+
+def _fp64_grads(h, w, y, gout):
+    """lp and d(Σ gout·lp)/dh, /dW in fp64 from the bf16 operands."""
+    hd = h.double().to(DEV).requires_grad_(True)
+    wd = w.double().to(DEV).requires_grad_(True)
+    lp = torch.log_softmax(hd @ wd.t(), -1).gather(-1, y.to(DEV)[:, None]).squeeze(-1)
+    (lp * gout.double().to(DEV)).sum().backward()
+    return lp.detach(), hd.grad, wd.grad
+
+
+def _bf16_reference_grads(h, w, y, gout):
+    """The reference's own bf16 pipeline on the T5 path: bf16 logits (lm_head output), bf16
+    log_softmax + gather (modeling.py:37-41) and autograd in bf16."""
+    hb = h.to(DEV).requires_grad_(True)
+    wb = w.to(DEV).requires_grad_(True)
+    lp = orc.logprobs_from_logits(hb @ wb.t(), y.to(DEV))
+    (lp * gout.to(DEV).to(lp.dtype)).sum().backward()
+    return hb.grad, wb.grad
+
+
+@pytest.mark.parametrize("N,H,V", [(111, 768, 1000), (64, 512, 33), (300, 768, 50257), (129, 512, 32128)])
+def test_lm_head_logprobs_autograd(N, H, V):
+    h, w, y = _operands(N, H, V, N + V)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(3))
+    hg = h.to(DEV).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32)
+    (lp * gout.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
+    torch.testing.assert_close(lp.detach().double(), lp64, rtol=1e-5, atol=2e-5)
+    assert hg.grad.dtype == torch.bfloat16 and wg.grad.dtype == torch.bfloat16
+    bh, bw = _bf16_reference_grads(h, w, y, gout)
+    eh, ew = _rel(hg.grad, dh64), _rel(wg.grad, dw64)
+    rh, rw = _rel(bh, dh64), _rel(bw, dw64)
+    assert eh < 1e-2 and ew < 1e-2, (eh, ew)
+    assert eh <= 2 * rh and ew <= 2 * rw, (eh, rh, ew, rw)
+
+
+def test_lm_head_logprobs_restart_on_large_logit_jump():
+    """Vocab rows from the 6th tile on get logits ~80 above the first tile's: the forward's
+    fixed exponent offset (the first tile's max) would overflow, so the workgroups rerun
+    their split with the true max (k_lmloss_fwd pass 2)."""
+    N, H, V = 96, 768, 2048
+    h, w, y = _operands(N, H, V, 11)
+    hf = h.float()
+    wf = w.float()
+    d = hf.mean(0)
+    wf[5 * 32:] += 80.0 * d / (d @ d)  # x_tv += ~80 on those rows for every token
+    w = wf.to(torch.bfloat16)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(4))
+    hg = h.to(DEV).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32)
+    (lp * gout.to(DEV)).sum().backward()
+    lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
+    assert torch.isfinite(lp).all() and torch.isfinite(hg.grad.float()).all()
+    torch.testing.assert_close(lp.detach().double(), lp64, rtol=1e-5, atol=1e-4)
+    assert _rel(hg.grad, dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
+
+
+def _ppo_inputs(B, T, V, H, seed, masked):
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(B, T, H, generator=g).to(torch.bfloat16)
+    w = (torch.randn(V, H, generator=g) * 0.05).to(torch.bfloat16)
+    ref_h = (h.float() + 0.1 * torch.randn(B, T, H, generator=g)).to(torch.bfloat16)
+    new_h = (h.float() + 0.05 * torch.randn(B, T, H, generator=g)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, T), generator=g)
+    old_values = torch.randn(B, T, generator=g)
+    values = old_values + 0.3 * torch.randn(B, T, generator=g)
+    scores = torch.rand(B, generator=g) * 24 - 12
+    lengths = mask = None
+    if masked:
+        lengths = torch.randint(1, T + 1, (B,), generator=g)
+        lengths[0] = T
+        mask = (torch.arange(T)[None, :] < lengths[:, None]).long()
+        old_values = old_values.masked_fill(mask == 0, 0)
+    return dict(h=h, w=w, ref_h=ref_h, new_h=new_h, labels=labels, old_values=old_values, values=values,
+                scores=scores, lengths=lengths, mask=mask)
+
+
+def _oracle_loss_side(x, lp_old, adv_w, ret, mask):
+    """The reference loss side on the device in fp32: logits from the bf16 operands, the
+    oracle's logprobs_from_logits and ppo_loss, autograd to (h, W, values)."""
+    B, T, H = x["new_h"].shape
+    hd = x["new_h"].float().to(DEV).requires_grad_(True)
+    wd = x["w"].float().to(DEV).requires_grad_(True)
+    vd = x["values"].to(DEV).requires_grad_(True)
+    lp = orc.logprobs_from_logits(hd @ wd.t(), x["labels"].to(DEV))
+    m = torch.ones(B, T, dtype=torch.long, device=DEV) if mask is None else mask.to(DEV)
+    loss, stats = orc.ppo_loss(lp, vd, lp_old.to(DEV), x["old_values"].to(DEV), adv_w.to(DEV), ret.to(DEV), m)
+    loss.backward()
+    return loss.detach(), stats, lp.detach(), hd.grad, wd.grad, vd.grad
+
+
+@pytest.mark.parametrize("B,T,V,H,masked", [(4, 9, 1031, 768, False), (16, 48, 32128, 768, True),
+                                            (128, 48, 50257, 768, False), (256, 48, 32128, 768, True),
+                                            (8, 20, 5000, 512, True)])
+def test_hot_path_loss_from_hidden_vs_oracle(B, T, V, H, masked):
+    """PPOHotPath.step_from_hidden (fused experience lm_head + GAE, then the fused loss side)
+    against the oracle's loss side on the product's own experience outputs (lp_old, whitened
+    advantages, returns are checked by the experience tests); C2 and C3 shapes included.
+    Masked tokens' hidden rows are NaN: the compacted loss side never reads them."""
+    x = _ppo_inputs(B, T, V, H, 100 + B + T, masked)
+    cfg = P.PPOConfig()
+    hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in x.items()}
+    if masked:  # the device copy only: the oracle below uses the clean rows
+        d["new_h"] = d["new_h"].masked_fill((d["mask"] == 0)[..., None], float("nan"))
+    loss, stats, dh, dw, dv = hp.step_from_hidden(d["h"], d["w"], d["ref_h"], d["w"], d["new_h"], d["labels"],
+                                                 d["old_values"], d["values"], d["scores"], lengths=d["lengths"],
+                                                 mask=d["mask"], route="fused")
+    torch.cuda.synchronize()
+    # the whitened advantages the loss saw: the GAE record of this step (unbiased, no group)
+    st = hp.adv_stats.cpu()
+    mu, var = P.modeling.moments_to_mean_var(st, unbiased=True)
+    adv_w = ((hp.adv_raw.cpu().double() - mu) * torch.rsqrt(var + 1e-8)).float()
+    want_loss, want_stats, want_lp, want_dh, want_dw, want_dv = _oracle_loss_side(
+        x, hp.lp_old.cpu(), adv_w, hp.returns.cpu(), x["mask"])
+    m = torch.ones(B, T, dtype=torch.bool) if x["mask"] is None else x["mask"].bool()
+    torch.testing.assert_close(hp.lp_new.cpu()[m], want_lp.cpu()[m], rtol=1e-5, atol=2e-5)
+    if x["mask"] is not None:
+        assert (hp.lp_new.cpu()[~m] == 0).all() and (dh.cpu()[~m] == 0).all()
+    torch.testing.assert_close(loss.cpu().reshape(()), want_loss.cpu(), rtol=1e-4, atol=1e-5)
+    got_stats = dict(zip(P.STATS_KEYS, stats.cpu().tolist()))
+    for k in P.STATS_KEYS:
+        assert got_stats[k] == pytest.approx(float(want_stats[k]), rel=1e-4, abs=1e-5), k
+    torch.testing.assert_close(dv.cpu(), want_dv.cpu(), rtol=1e-5, atol=1e-6)
+    assert torch.isfinite(dh.float()).all() and torch.isfinite(dw.float()).all()
+    eh, ew = _rel(dh.cpu()[m], want_dh.cpu()[m]), _rel(dw.cpu(), want_dw.cpu())
+    assert eh < 1e-2 and ew < 1e-2, (eh, ew)
+
+
+def test_loss_from_hidden_deterministic_and_drop_in():
+    """Two identical calls give the same bits (fixed-order sums, no atomics); the drop-in
+    PPOConfig.loss_from_hidden (autograd through lm_head_logprobs + loss) matches the fused
+    hot path's gradients to bf16 rounding."""
+    B, T, V, H = 8, 24, 3000, 768
+    x = _ppo_inputs(B, T, V, H, 77, True)
+    d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in x.items()}
+    outs = []
+    for _ in range(2):
+        hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+        o = hp.step_from_hidden(d["h"], d["w"], d["ref_h"], d["w"], d["new_h"], d["labels"], d["old_values"],
+                                d["values"], d["scores"], lengths=d["lengths"], mask=d["mask"], route="fused")
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in o])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # drop-in: whiten the hot path's raw advantages the same way, then autograd
+    st = hp.adv_stats
+    mu, var = P.modeling.moments_to_mean_var(st, unbiased=True)
+    adv_w = ((hp.adv_raw.double() - mu) * torch.rsqrt(var + 1e-8)).float()
+    hg = d["new_h"].clone().requires_grad_(True)
+    wg = d["w"].clone().requires_grad_(True)
+    vg = d["values"].clone().requires_grad_(True)
+    loss, stats = P.PPOConfig().loss_from_hidden(hg, wg, vg, d["labels"], hp.lp_old, d["old_values"], adv_w,
+                                                hp.returns, d["mask"])
+    loss.backward()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss.reshape(()), outs[0][0].reshape(()), rtol=1e-5, atol=1e-6)
+    m = d["mask"].bool()
+    assert _rel(hg.grad[m], outs[0][2][m]) < 5e-3 and _rel(wg.grad, outs[0][3]) < 5e-3
+    torch.testing.assert_close(vg.grad, outs[0][4], rtol=1e-5, atol=1e-6)

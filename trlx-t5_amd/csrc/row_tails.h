@@ -226,11 +226,15 @@ __global__ __launch_bounds__(kRolloutThreads) void k_rollout_gae(GaeRolloutArgs 
 
 // The split-beta whitening coefficients as a launch of its own (one thread): the serial
 // split schedule, and the last batch of a pipelined sequence (nothing left to fold it into).
+// (The two non-template kernels of this header are defined in the one translation unit that
+// launches them, vocab_rows.hip; other includers define TRLX_ROW_TAILS_NO_KERNELS.)
+#ifndef TRLX_ROW_TAILS_NO_KERNELS
 __global__ void k_whiten_coef(const double* stats, int unbiased, const double* ctl_state, float host_beta,
                               float* coef) {
     if (threadIdx.x == 0)
         whiten_coef_split(stats, unbiased, ctl_state ? float(ctl_state[TRLX_CTL_KL_COEF]) : host_beta, coef);
 }
+#endif
 
 // ------------------------------------------------------------------ loss sums per rollout
 struct LossRolloutArgs {
@@ -347,9 +351,11 @@ __device__ __forceinline__ void loss_tail_block(const LossRolloutArgs& L, int bl
     }
 }
 
+#ifndef TRLX_ROW_TAILS_NO_KERNELS
 __global__ __launch_bounds__(kRolloutThreads) void k_rollout_loss(LossRolloutArgs L) {
     __shared__ double red[kRolloutsPerBlock * 16];
     loss_tail_block(L, int(blockIdx.x), int(gridDim.x), red);
 }
+#endif
 
 }  // namespace trlx

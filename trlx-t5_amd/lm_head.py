@@ -8,6 +8,12 @@ The [.., V] logits are never written to HBM: MFMA tiles of 256 tokens x 256 voca
 schedule; 128 x 128 for small N) keep them in registers and reduce each tile to a partial
 (max, Σexp) per token (csrc/lmhead_rows.hip).  PPOHotPath.experience_from_hidden runs the
 experience step this way.
+
+With gradients (hidden or weight requiring grad, H in {512, 768}) the same call is the loss
+side's differentiable block, accelerate_ppo_model.py:96-118 (lm_head + logprobs_from_logits +
+autograd back through both): csrc/lmhead_loss.hip's forward keeps lse and E_t = Σ_v p_tv·W_v
+per token, and the backward forms dh_t = g_t·(W[y_t] − E_t) and dW = Σ_t g_t·(onehot − p_t)·h_t
+by recomputing the logits tiles on MFMA — no [N, V] logits or dlogits in HBM either way.
 """
 import torch
 
@@ -15,13 +21,65 @@ from . import _lib
 
 __all__ = ["lm_head_logprobs"]
 
+GRAD_HIDDEN_SIZES = (512, 768)  # hidden sizes the fused backward is built for (lmhead_loss.hip)
+
+
+def _operands(hidden, weight, labels):
+    H = hidden.shape[-1]
+    h = hidden.reshape(-1, H)
+    if h.stride(-1) != 1 or h.stride(0) % 8 or h.data_ptr() % 16:
+        h = h.contiguous()
+    w = weight if (weight.stride(-1) == 1 and weight.stride(0) % 8 == 0 and weight.data_ptr() % 16 == 0) \
+        else weight.contiguous()
+    return h, w, labels.reshape(-1).contiguous()
+
+
+class _LmHeadLogprobs(torch.autograd.Function):
+    """lp = log_softmax(h·Wᵀ)[y] with its backward, logits never materialised."""
+
+    @staticmethod
+    def forward(ctx, hidden, weight, labels, out_dtype):
+        h, w, y = _operands(hidden, weight, labels)
+        N, H, V = h.shape[0], h.shape[1], w.shape[0]
+        dev = h.device
+        lp = torch.empty(N, dtype=out_dtype, device=dev)
+        lse = torch.empty(N, dtype=torch.float32, device=dev)
+        e = torch.empty((N, H), dtype=torch.float32, device=dev)
+        ws = torch.empty(_lib.query("trlx_lmhead_loss_workspace_bytes", N, H, V), dtype=torch.uint8, device=dev)
+        _lib.call("trlx_lmhead_logprobs_fwd_saved", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), N, H, V,
+                  y.data_ptr(), 1, lp.data_ptr(), _lib.dtype_code(lp), lse.data_ptr(), e.data_ptr(), ws.data_ptr(),
+                  _lib.stream_of(h))
+        ctx.save_for_backward(h, w, y, lse, e)
+        ctx.shapes = (hidden.shape, hidden.dtype, weight.shape, weight.dtype)
+        return lp.view(labels.shape)
+
+    @staticmethod
+    def backward(ctx, grad_lp):
+        h, w, y, lse, e = ctx.saved_tensors
+        hshape, hdt, wshape, wdt = ctx.shapes
+        N, H, V = h.shape[0], h.shape[1], w.shape[0]
+        dev = h.device
+        g = grad_lp.reshape(-1).contiguous()
+        if g.dtype not in (torch.float32, torch.bfloat16):
+            g = g.float()
+        dh = torch.empty((N, H), dtype=hdt, device=dev)
+        dw = torch.empty((V, H), dtype=wdt, device=dev)
+        ws = torch.empty(_lib.query("trlx_lmhead_loss_workspace_bytes", N, H, V), dtype=torch.uint8, device=dev)
+        _lib.call("trlx_lmhead_logprobs_bwd", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), N, H, V,
+                  y.data_ptr(), 1, g.data_ptr(), _lib.dtype_code(g), lse.data_ptr(), e.data_ptr(), dh.data_ptr(),
+                  dh.stride(0), _lib.dtype_code(dh), dw.data_ptr(), _lib.dtype_code(dw), dw.stride(0), ws.data_ptr(),
+                  _lib.stream_of(h))
+        return dh.view(hshape), dw.view(wshape), None, None
+
 
 def lm_head_logprobs(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor, out_dtype=None,
                      return_lse: bool = False):
     """hidden [..., H] bf16, weight [V, H] bf16 (nn.Linear.weight), labels [...] int64 ->
     logprobs [...] of out_dtype (default: hidden.dtype, the dtype the reference's logits —
     and so its logprobs — have).  Arithmetic: bf16 products, fp32 accumulation and
-    softmax statistics; the logits are not rounded to bf16 (the reference rounds them)."""
+    softmax statistics; the logits are not rounded to bf16 (the reference rounds them).
+    Differentiable w.r.t. hidden and weight when either requires grad (H in
+    GRAD_HIDDEN_SIZES): the backward runs lmhead_loss.hip's dh / dW passes."""
     _lib.require_cuda(hidden, weight, labels)
     if hidden.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
         raise TypeError("lm_head_logprobs takes bf16 hidden states and weight")
@@ -32,14 +90,15 @@ def lm_head_logprobs(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.T
         raise ValueError(f"weight must be [V, {H}], got {tuple(weight.shape)}")
     if tuple(labels.shape) != tuple(hidden.shape[:-1]):
         raise ValueError("labels must have hidden.shape[:-1]")
-    h = hidden.reshape(-1, H)
-    if h.stride(-1) != 1 or h.stride(0) % 8 or h.data_ptr() % 16:
-        h = h.contiguous()
-    w = weight if (weight.stride(-1) == 1 and weight.stride(0) % 8 == 0 and weight.data_ptr() % 16 == 0) \
-        else weight.contiguous()
-    y = labels.reshape(-1).contiguous()
-    N, V = h.shape[0], w.shape[0]
     dt = hidden.dtype if out_dtype is None else out_dtype
+    if torch.is_grad_enabled() and (hidden.requires_grad or weight.requires_grad):
+        if H not in GRAD_HIDDEN_SIZES:
+            raise ValueError(f"lm_head_logprobs with gradients: hidden size {H} not built {GRAD_HIDDEN_SIZES}")
+        if return_lse:
+            raise ValueError("return_lse is for the no-grad (experience) path")
+        return _LmHeadLogprobs.apply(hidden, weight, labels, dt)
+    h, w, y = _operands(hidden, weight, labels)
+    N, V = h.shape[0], w.shape[0]
     lp = torch.empty(N, dtype=dt, device=h.device)
     lse = torch.empty(N, dtype=torch.float32, device=h.device) if return_lse else None
     ws = torch.empty(_lib.query("trlx_lmhead_workspace_bytes", N, V), dtype=torch.uint8, device=h.device)

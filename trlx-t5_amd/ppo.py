@@ -16,6 +16,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+from .lm_head import lm_head_logprobs
 from .modeling import (RunningMoments, _allreduce_moments, _token_geometry, flatten_dict,
                        grad_buffer_like, whiten)
 
@@ -322,6 +323,19 @@ class PPOConfig:
         loss, stats = _PPOLoss.apply(logprobs, values, old_logprobs, old_values, advantages, returns, mask,
                                      self.cliprange, self.cliprange_value, self.vf_coef)
         return loss, stats_dict(stats)
+
+    def loss_from_hidden(self, hidden, weight, values, labels, old_logprobs, old_values, advantages, returns,
+                         mask=None):
+        """The loss side from the policy's last hidden states:
+            self.loss(logprobs_from_logits(hidden @ weight.T, labels), values, ...)
+        (accelerate_ppo_model.py:96-118 with the lm_head of ppo_models.py:640 / :274), the
+        [.., V] logits and dlogits never in HBM: lm_head_logprobs' differentiable MFMA block
+        feeds the PPO loss kernels, and backward() delivers d hidden, d weight (lm_head) and
+        d values.  hidden [.., H] / weight [V, H] bf16, H in lm_head.GRAD_HIDDEN_SIZES.
+        Returns (loss, stats) like loss(); logprobs are kept in fp32 (the reference's bf16
+        logits give bf16 logprobs)."""
+        lp = lm_head_logprobs(hidden, weight, labels, out_dtype=torch.float32)
+        return self.loss(lp, values, old_logprobs, old_values, advantages, returns, mask)
 
     def loss_from_logits(self, logits, values, labels, old_logprobs, old_values, advantages, returns,
                          mask=None, adv_stats=None, unbiased=True, return_device_stats=False):

@@ -637,17 +637,24 @@ class PPOHotPath:
                       _lib.dtype_code(self.returns), *grads, s.cuda_stream)
             tail_stats = self.adv_stats.data_ptr()
         self._ev_end("loss", s)
+        self._loss_tail(s, tail_stats)
+        return self.loss, self.stats, self.dlogits, self.dvalues
+
+    def _loss_tail(self, s, tail_stats):
+        """The loss tail after a loss launch (fixed-order sums of the token records -> loss + 13
+        stats, + the KL-controller update): deferred into the next experience launch, on the
+        side stream, or its own launch."""
         ts = s
         if self.tail_stream is not None:
             rows_done = self._next_event()
             rows_done.record(s)
             ts = self.tail_stream
             rows_done.wait(ts)
-        args = (B, T, tail_stats, float(self.cfg.vf_coef), self.loss.data_ptr(), self.stats.data_ptr(),
+        args = (self.B, self.T, tail_stats, float(self.cfg.vf_coef), self.loss.data_ptr(), self.stats.data_ptr(),
                 self.workspace.data_ptr())
         if self.defer_tail:  # runs inside the next experience launch (or wait_stats)
             self._tail_pending = args
-            return self.loss, self.stats, self.dlogits, self.dvalues
+            return
         self._ev("rollout_loss", ts)
         if self.ctl is not None:  # + kl_ctl.update(approx_kl) (accelerate_ppo_model.py:123,130-131)
             _lib.call("trlx_ppo_rollout_loss_ctl", *args, self.ctl.kl_ctl(), ts.cuda_stream)
@@ -657,7 +664,78 @@ class PPOHotPath:
         if self.tail_stream is not None:
             self.tail_done = self._next_event()
             self.tail_done.record(ts)
-        return self.loss, self.stats, self.dlogits, self.dvalues
+
+    # -------------------------------------------------------------- K2 from hidden states (§8f-2, loss side)
+    LOSS_FROM_HIDDEN_SIZES = (512, 768)
+
+    def policy_loss_from_hidden(self, hidden, weight, labels, values, old_values, mask=None,
+                                grad_dtype=torch.bfloat16):
+        """K2 with the lm_head folded in (loss side): the policy's last hidden
+        states [B, T, H] and lm_head weight [V, H] (bf16, H in LOSS_FROM_HIDDEN_SIZES) replace
+        the logits — the reference's policy forward + logprobs_from_logits + PPO loss +
+        autograd back through the lm_head (accelerate_ppo_model.py:96-118, ppo_models.py:640 /
+        :274) without [B, T, V] logits or dlogits in HBM (trlx_ppo_loss_from_hidden: three MFMA
+        launches and a per-token combine; tokens with mask == 0 are compacted out).  Returns
+        (loss, stats, dhidden [B, T, H], dweight [V, H], dvalues), gradients in grad_dtype;
+        the same loss tail (deferred / side stream) as policy_loss.  Unsplit whitening only (the
+        serial step(): experience / experience_from_hidden, then this)."""
+        if self._split_mode:
+            raise RuntimeError("policy_loss_from_hidden runs after the unsplit GAE (step / experience); "
+                               "split-beta / pipelined batches use policy_loss")
+        B, T, V = self.B, self.T, self.V
+        if hidden.dim() != 3 or tuple(hidden.shape[:2]) != (B, T) or weight.dim() != 2 or weight.shape[0] != V or \
+                weight.shape[1] != hidden.shape[2] or hidden.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+            raise ValueError(f"hidden {tuple(hidden.shape)}/{hidden.dtype} and weight {tuple(weight.shape)}/"
+                             f"{weight.dtype} do not match the hot path ({B},{T},H) x ({V},H) bf16")
+        H = hidden.shape[2]
+        if H not in self.LOSS_FROM_HIDDEN_SIZES:
+            raise ValueError(f"policy_loss_from_hidden: hidden size {H} not built {self.LOSS_FROM_HIDDEN_SIZES}")
+        if grad_dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("grad_dtype must be bf16 or fp32")
+        _lib.require_cuda(hidden, weight)
+        labels = self._int64(labels, (B, T), "labels")
+        mask = self._int64(mask, (B, T), "mask", required=False)
+        values = self._vec(values, (B, T), "values")
+        old_values = self._vec(old_values, (B, T), "old_values")
+        h = hidden.reshape(B * T, H)
+        if h.stride(1) != 1 or h.stride(0) % 8 or h.data_ptr() % 16:
+            h = h.contiguous()
+        w = weight if (weight.stride(1) == 1 and weight.stride(0) % 8 == 0 and weight.data_ptr() % 16 == 0) \
+            else weight.contiguous()
+        N = B * T
+        if getattr(self, "dhidden", None) is None or self.dhidden.shape != (B, T, H) or self.dhidden.dtype != grad_dtype:
+            self.dhidden = torch.empty((B, T, H), dtype=grad_dtype, device=self.device)
+            self.dweight = torch.empty((V, H), dtype=grad_dtype, device=self.device)
+        nbytes = _lib.query("trlx_lmhead_loss_workspace_bytes", N, H, V)
+        if getattr(self, "lm_loss_ws", None) is None or self.lm_loss_ws.numel() < nbytes:
+            self.lm_loss_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        s = torch.cuda.current_stream(self.device)
+        self._launch_pending_tail(s)
+        if self.tail_done is not None:
+            self.tail_done.wait(s)
+        dh, dw = self.dhidden, self.dweight
+        self._ev("loss", s)
+        _lib.call("trlx_ppo_loss_from_hidden", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), B, T, H, V,
+                  labels.data_ptr(), self.lp_old.data_ptr(), _lib.F32, self.adv_raw.data_ptr(),
+                  self.adv_stats.data_ptr(), 0 if self.distributed else 1, _lib.ptr(mask), values.data_ptr(),
+                  _lib.dtype_code(values), old_values.data_ptr(), _lib.dtype_code(old_values), self.returns.data_ptr(),
+                  _lib.dtype_code(self.returns), float(self.cfg.cliprange), float(self.cfg.cliprange_value),
+                  float(self.cfg.vf_coef), self.lp_new.data_ptr(), dh.data_ptr(), H, _lib.dtype_code(dh), dw.data_ptr(),
+                  _lib.dtype_code(dw), H, self.dvalues.data_ptr(), self.workspace.data_ptr(),
+                  self.lm_loss_ws.data_ptr(), s.cuda_stream)
+        self._ev_end("loss", s)
+        self._loss_tail(s, self.adv_stats.data_ptr())
+        return self.loss, self.stats, dh, dw, self.dvalues
+
+    def step_from_hidden(self, hidden, weight, ref_hidden, ref_weight, new_hidden, labels, old_values, values,
+                         scores, lengths=None, mask=None, group=None, route="auto", new_weight=None):
+        """step() from hidden states on both sides: experience_from_hidden
+        (policy + reference lm_head + logprobs, GAE) then policy_loss_from_hidden on the
+        updated policy's hidden states (new_weight: its lm_head, default `weight`)."""
+        self.experience_from_hidden(hidden, weight, ref_hidden, ref_weight, labels, old_values, scores,
+                                    lengths=lengths, mask=mask, group=group, route=route)
+        return self.policy_loss_from_hidden(new_hidden, weight if new_weight is None else new_weight, labels, values,
+                                            old_values, mask=mask)
 
     def release_lm_logits(self):
         """Free the gemm route's [2, chunk, T, V] logits ring (re-allocated on next use)."""
