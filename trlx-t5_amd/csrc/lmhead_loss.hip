@@ -44,12 +44,8 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 constexpr int kLLRows = 32;            // rows of a staged tile: vocab rows (forward) / tokens (dW)
-constexpr int kLLThreads = 256;        // 2 pairs x 2 hidden halves
-constexpr int kLLTokTile = 64;         // tokens per forward workgroup (2 pairs x 32)
-constexpr int kLLVocTile = 64;         // vocab rows per dW workgroup
 constexpr int kLLMaxSplits = 8;        // vocab splits of the forward (workspace sizing)
 constexpr float kLLOverflow = 60.0f;   // logit - offset bound of the fixed-offset softmax (e^60)
-constexpr int kLLXchg = 4 * 4096;      // partial-S exchange: 16 fp32 per lane per wave
 
 enum LmLossMode { kLLPpo = 0, kLLFwd = 1, kLLBwd = 2 };
 
@@ -71,6 +67,7 @@ struct LmLossArgs {
     float* nlse;     // [N] -lse·log2e (compact; read by the dW kernel)
     float* gbuf;     // [N] d loss / d lp (compact)
     int* ybuf;       // [N] label (compact)
+    int* flags;      // [forward grid][waves] 1 = the wave's fixed offset overflowed (k_lmloss_fwd)
     float* ebuf;     // kLLFwd: E = O / l written here; kLLBwd: read ([N, H], token rows)
     float* lse_io;   // kLLFwd: lse out; kLLBwd: lse in (token rows); may be NULL in kLLPpo
     void* lp;        // lp out (token rows; kLLPpo: fp32 lp_out)
@@ -111,40 +108,67 @@ struct LmLossArgs {
 };
 
 // ------------------------------------------------------------------ staged tile image
-// A [32 rows][H] bf16 tile as H/128 segments of [32 rows][256 B]; 16-B chunk c of a row sits at
-// chunk c ^ key(row) of its segment row (cdna_hip_programming.md T10, image (b)): the row reads
-// of the 32x32x16 operand (32 rows x one 16-B chunk per half-wave) and the transposed reads
-// (4 rows x 16 columns per 16-lane group) are both conflict-free.
-__device__ __forceinline__ int ll_key(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+// A [32 rows][H] bf16 tile as H/128 segments of [32 rows][128 columns] (8 KB), each in the
+// 8-row x 32-column subtile image of cdna_hip_programming.md T10 (a): 16-B chunk ch of row r sits
+// at 2048·(r>>3) + 512·(ch>>2) + 64·(r&7) + 16·((ch&3) ^ ((r>>2)&3)).  The row reads of the
+// 32x32x16 operand (32 rows x one 16-B chunk per half-wave) and the transposed reads (4 rows x 16
+// columns per 16-lane group) are conflict-free, and the XOR touches only the low 2 bits of the
+// chunk: every transposed read of a lane is one of 2 base addresses plus an immediate (column
+// block, k-step, segment), every row read one of 2 bases plus an immediate.
 __device__ __forceinline__ int ll_off(int r, int d) {
-    return (d >> 7) * 8192 + r * 256 + ((((d >> 3) & 15) ^ ll_key(r)) << 4) + ((d & 7) << 1);
+    const int ch = (d >> 3) & 15;
+    return (d >> 7) * 8192 + 2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3)) +
+           ((d & 7) << 1);
+}
+// The tile row that lane `lane` of DMA piece i fills (piece i: segment i >> 3, 8-row group
+// (i & 7) >> 1, subtile pair i & 1).
+__device__ __forceinline__ int ll_piece_row(int i, int lane) { return 8 * ((i & 7) >> 1) + ((lane >> 2) & 7); }
+// One 1-KB LDS-DMA piece of a tile: lane l lands at the piece's byte 16·l, so it fetches the
+// logical chunk that the image puts there.  Buffer-resource form (`row_bytes` = the byte offset
+// of the lane's row in the resource): hipcc then tracks these LDS writes like the s2 lm_head
+// kernel's and does not put a vmcnt(0) in front of the next LDS read (the flat
+// global_load_lds form made every tile wait for the DMA of the NEXT one before its first read).
+__device__ __forceinline__ void ll_piece(char* slot, int i, __amdgpu_buffer_rsrc_t rs, int row_bytes, int lane) {
+    const int r = ll_piece_row(i, lane);
+    const int ch = 4 * (2 * (i & 1) + (lane >> 5)) + ((lane & 3) ^ ((r >> 2) & 3));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
+                                             row_bytes + (i >> 3) * 256 + ch * 16, 0, 0, 0);
 }
 
-// One 1-KB LDS-DMA piece of a tile: piece i = segment i >> 3, rows 4(i & 7) .. +3; lane l
-// lands at slot (row 4(i&7) + l/16, chunk l&15) and fetches the logical chunk (l&15) ^ key.
-// `src_row` = the global row pointer of the lane's tile row.
-__device__ __forceinline__ void ll_piece(char* slot, int i, const uint16_t* src_row, int lane) {
-    const int r = 4 * (i & 7) + (lane >> 4);
-    const int c = (lane & 15) ^ ll_key(r);
-    __builtin_amdgcn_global_load_lds(src_row + (i >> 3) * 128 + c * 8,
-                                     (__attribute__((address_space(3))) void*)(slot + i * 1024), 16, 0, 0);
+// Per-lane byte offsets of the two operand reads inside a staged tile, for a wave whose hidden
+// slice starts on a segment boundary (d0 % 128 == 0): every read is then one of these lane bases
+// plus a wave-uniform offset d0·64 plus a compile-time immediate (no per-read address VALU).
+//   row read, k-step k (32x32x16 A operand by rows: lane -> tile row l&31, columns d0 + 16k + 8hi):
+//     d0·64 + (k>>3)·8192 + ((k&7)>>1)·512 + row[k&1]
+//   transposed read (k-step s, column block b, tile rows 16s + 4hi + q + 8·p8, columns
+//     d0 + 32b + 16(g&1) + 4p for lane 16g + 4q + p):  d0·64 + (b>>2)·8192 + (b&3)·512 + 4096·s + tr[p8]
+struct LlLane {
+    int row[2];
+    int tr[2];
+};
+__device__ __forceinline__ LlLane ll_lane(int lane) {
+    LlLane L;
+    const int r = lane & 31, hi = lane >> 5;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        const int ch = 2 * par + hi;
+        L.row[par] = 2048 * (r >> 3) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
+    }
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int ch = 2 * (g & 1) + (p >> 1);
+#pragma unroll
+    for (int p8 = 0; p8 < 2; ++p8)
+        L.tr[p8] = 2048 * p8 + 64 * (4 * hi + q) + 16 * (ch ^ (hi + 2 * p8)) + 8 * (p & 1);
+    return L;
 }
-
-// Row read of the 32x32x16 operand: lane l -> tile row l&31, 8 elements from column d0 + 8·(l>>5).
-__device__ __forceinline__ bf16x8_t ll_row_frag(const char* slot, int lane, int d0) {
-    return *reinterpret_cast<const bf16x8_t*>(slot + ll_off(lane & 31, d0 + 8 * (lane >> 5)));
+__device__ __forceinline__ bf16x8_t ll_row_frag(const char* slice, const LlLane& L, int k) {
+    return *reinterpret_cast<const bf16x8_t*>(slice + (k >> 3) * 8192 + ((k & 7) >> 1) * 512 + L.row[k & 1]);
 }
-
-// Transposed read of the 32x32x16 operand whose k runs over 16 tile rows in the order of an
-// S accumulator used as the other operand (k-step s: element j of lane half hi is tile row
-// 16s + 8(j>>2) + 4hi + (j&3)), column dcol0 + (l & 31): two ds_read_b64_tr_b16.
-__device__ __forceinline__ bf16x8_t ll_tr_frag(const char* slot, int lane, int s, int dcol0) {
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    const int r0 = 16 * s + 4 * (lane >> 5) + q;
-    const int d = dcol0 + 16 * (g & 1) + 4 * p;
+__device__ __forceinline__ bf16x8_t ll_tr_frag(const char* slice, const LlLane& L, int s, int b) {
     typedef __attribute__((address_space(3))) s16x4_t lds_s4;
-    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(slot + ll_off(r0, d)));
-    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(slot + ll_off(r0 + 8, d)));
+    const char* base = slice + (b >> 2) * 8192 + (b & 3) * 512 + 4096 * s;
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + L.tr[0]));
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + L.tr[1]));
     const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     return __builtin_bit_cast(bf16x8_t, v);
 }
@@ -156,140 +180,231 @@ __device__ __forceinline__ bf16x8_t pack8(const float* p) {
     return r;
 }
 
-// The two waves of a pair add their partial S tiles (each over its hidden half) through LDS:
-// every lane ends with the full sum of its 16 elements (fp32 addition commutes, so both waves
-// hold the same bits).  Barrier inside: every wave of the workgroup must call it.
-__device__ __forceinline__ void ll_pair_sum(f32x16_t& s, char* xbuf, int wave, int lane) {
+// Scheduling masks of __builtin_amdgcn_sched_group_barrier (LLVM AMDGPU): MFMA, DS read.
+constexpr int kSgMfma = 0x008, kSgDsRead = 0x100;
+
+// S tile of one wave over its hidden slice: KS MFMAs whose streamed operand is read by rows.
+// Pipelined by sched groups: 3 reads ahead, then (1 MFMA, 1 read) pairs — left to itself the
+// compiler issued each read right before its MFMA and waited for it (LDS latency every step).
+template <int KS>
+__device__ __forceinline__ f32x16_t ll_s_product(const char* slice, const LlLane& L, const bf16x8_t* regs) {
+    f32x16_t s = f32x16_t{};
+    bf16x8_t af[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) af[k] = ll_row_frag(slice, L, k);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k], regs[k], s, 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(kSgDsRead, 3, 0);
+#pragma unroll
+    for (int k = 0; k < KS - 3; ++k) {
+        __builtin_amdgcn_sched_group_barrier(kSgMfma, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(kSgDsRead, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(kSgMfma, 3, 0);
+    return s;
+}
+// The second product over the wave's slice: OB blocks of 32 hidden columns x 2 k-steps, the
+// staged tile read transposed (4 reads per block); LEFT: the register operand is the A operand
+// (dW = dSᵀ·h), else the B operand (Oᵀ = Wᵀ·Pᵀ).  Pipelined one block ahead.
+template <int OB, bool LEFT>
+__device__ __forceinline__ void ll_tr_product(const char* slice, const LlLane& L, bf16x8_t r0, bf16x8_t r1,
+                                              f32x16_t* acc) {
+    bf16x8_t t[OB][2];
+#pragma unroll
+    for (int b = 0; b < OB; ++b) {
+        t[b][0] = ll_tr_frag(slice, L, 0, b);
+        t[b][1] = ll_tr_frag(slice, L, 1, b);
+    }
+#pragma unroll
+    for (int b = 0; b < OB; ++b) {
+        if (LEFT) {
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r0, t[b][0], acc[b], 0, 0, 0);
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(r1, t[b][1], acc[b], 0, 0, 0);
+        } else {
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t[b][0], r0, acc[b], 0, 0, 0);
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t[b][1], r1, acc[b], 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_sched_group_barrier(kSgDsRead, 8, 0);
+#pragma unroll
+    for (int b = 0; b < OB - 2; ++b) {
+        __builtin_amdgcn_sched_group_barrier(kSgMfma, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(kSgDsRead, 4, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(kSgMfma, 4, 0);
+}
+
+// The NW waves of a group add their partial S tiles (each over its slice of the hidden
+// dimension) through LDS, in the fixed order of their slice index, so every wave of the group
+// ends with the same bits.  Barrier inside: every wave of the workgroup must call it.
+template <int NW>
+__device__ __forceinline__ void ll_group_sum(f32x16_t& s, char* xbuf, int wave, int lane) {
     f32x4_t* mine = reinterpret_cast<f32x4_t*>(xbuf + wave * 4096);
 #pragma unroll
     for (int q = 0; q < 4; ++q) mine[q * 64 + lane] = f32x4_t{s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]};
     __syncthreads();
-    const f32x4_t* oth = reinterpret_cast<const f32x4_t*>(xbuf + (wave ^ 1) * 4096);
+    const f32x4_t* o = reinterpret_cast<const f32x4_t*>(xbuf + (wave - wave % NW) * 4096);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const f32x4_t o = oth[q * 64 + lane];
-        s[4 * q] += o.x;
-        s[4 * q + 1] += o.y;
-        s[4 * q + 2] += o.z;
-        s[4 * q + 3] += o.w;
+    for (int q = 0; q < 4; ++q) {  // own slice read back too: nothing of s stays live across the barrier
+        f32x4_t v[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) v[j] = o[j * 256 + q * 64 + lane];  // 4 KB (256 x 16 B) per wave
+#pragma unroll
+        for (int j = 1; j < NW; ++j) v[0] += v[j];
+        s[4 * q] = v[0].x; s[4 * q + 1] = v[0].y; s[4 * q + 2] = v[0].z; s[4 * q + 3] = v[0].w;
+        __builtin_amdgcn_sched_barrier(0);  // 4 reads in flight at a time (registers)
     }
 }
 
+// Workgroup geometry: NG groups of NW waves; a group owns 32 tokens (forward) / 32 vocab rows
+// (dW); wave q of a group holds hidden slice [q·H/NW, (q+1)·H/NW): its h / W fragments
+// (H/NW/16 registers x 4) and its slice of O / dW (H/NW/32 blocks x 16 accumulators).
+template <int H_, int NG_, int NW_>
+struct LlGeom {
+    static constexpr int H = H_, NG = NG_, NW = NW_;
+    static constexpr int kWaves = NG * NW, kThreads = kWaves * 64;
+    static constexpr int HS = H / NW, KS = HS / 16, OB = HS / 32;
+    static constexpr int kPieces = H / 16, NI = kPieces / kWaves;  // 1-KB DMA pieces per tile / per wave
+    static constexpr int kStage = kLLRows * H * 2;
+    static_assert(kPieces % kWaves == 0 && HS % 128 == 0, "geometry: slices start on 128-column segments");
+    static_assert(kWaves <= 4, "forward overflow flags: 4 words per workgroup (ll_carve)");
+};
+// 4 waves (one per SIMD, 512 registers each): at H = 768 a wave holds 96 h / W fragment
+// registers and 192 accumulators; an 8-wave 4-slice layout (2 waves per SIMD, 256 registers)
+// spilled the fragments at every tile, and its 192-column slices do not start on segments.
+typedef LlGeom<768, 2, 2> LlG768;
+typedef LlGeom<512, 2, 2> LlG512;
+
 // ------------------------------------------------------------------ forward (flash-O)
-// Workgroup = 64 tokens x one vocab split; wave (pair pr, half hh).  Per 32-row vocab tile:
-//   S^T[v][t] = Σ_d W[v][d]·h[t][d]   (24 MFMAs over the wave's half, pair sum through LDS)
+// Workgroup = NG·32 tokens x one vocab split; wave (group g, slice q).  Per 32-row vocab tile:
+//   S^T[v][t] = Σ_d W[v][d]·h[t][d]   (KS MFMAs over the wave's hidden slice, group sum in LDS)
 //   P = exp(S - offset) per token (lanes t and t^32 hold its 32 values), Σ P, label logit
-//   O^T[d][t] += Σ_v W[v][d]·P[t][v] (12 d-blocks x 2 k-steps: W read transposed, P = the S
+//   O^T[d][t] += Σ_v W[v][d]·P[t][v] (OB d-blocks x 2 k-steps: W read transposed, P = the S
 //   accumulator converted to bf16 as the B operand): each lane's O registers are ONE token's.
-template <int KH>
-__global__ __launch_bounds__(kLLThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
-    constexpr int HW = 16 * KH, H = 2 * HW, OB = HW / 32, NI = H / 64;
-    constexpr int kStage = kLLRows * H * 2;
-    __shared__ __attribute__((aligned(16))) char smem[2 * kStage + kLLXchg];
+// 8 waves (2 per SIMD) at H = 768: 48 + 96 fragment / accumulator registers per wave leave the
+// compiler room to keep LDS reads in flight ahead of the MFMAs (a 4-wave, 2-slice layout at
+// 96 + 192 registers serialised every ds_read with its MFMA).
+template <class G, bool RESTART>
+__global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
+    constexpr int HS = G::HS, KS = G::KS, OB = G::OB, NI = G::NI, kStage = G::kStage;
+    __shared__ __attribute__((aligned(16))) char smem[2 * kStage + G::kWaves * 4096];
     char* xbuf = smem + 2 * kStage;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, pr = wave >> 1, hh = wave & 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave / G::NW, sq = wave % G::NW;
     const int hi = lane >> 5, c32 = lane & 31;
+    const LlLane LL = ll_lane(lane);
     const int nv = a.rows ? *a.nrows : a.N;
     const int split = int(blockIdx.x) % a.nsplit, mt = int(blockIdx.x) / a.nsplit;
-    const int m0 = mt * kLLTokTile;
+    const int m0 = mt * 32 * G::NG;
     if (m0 >= nv) return;  // past the compacted tokens (the grid's last blocks)
-    const int tm = m0 + pr * 32 + c32;
+    const int tm = m0 + grp * 32 + c32;
     const bool valid = tm < nv;
     const int tc = valid ? tm : nv - 1;
     const int row = a.rows ? a.rows[tc] : tc;
     const int64_t y = valid ? a.labels[int64_t(row) * a.lb] : -1;
-    bf16x8_t hf[KH];  // B operand of S^T: lane -> token c32, hidden hh·HW + 16ks + 8hi + j
+    bf16x8_t hf[KS];  // B operand of S^T: lane -> token c32, hidden sq·HS + 16ks + 8hi + j
     {
-        const uint16_t* hp = a.h + int64_t(row) * a.ldh + hh * HW + 8 * hi;
+        const uint16_t* hp = a.h + int64_t(row) * a.ldh + sq * HS + 8 * hi;
 #pragma unroll
-        for (int ks = 0; ks < KH; ++ks) hf[ks] = *reinterpret_cast<const bf16x8_t*>(hp + 16 * ks);
+        for (int ks = 0; ks < KS; ++ks) hf[ks] = *reinterpret_cast<const bf16x8_t*>(hp + 16 * ks);
     }
     const int nvt = (a.V + kLLRows - 1) / kLLRows;
     const int t0 = int(int64_t(split) * nvt / a.nsplit), t1 = int(int64_t(split + 1) * nvt / a.nsplit);
-    auto issue = [&](int t, char* slot) {
+    // W rows by buffer loads: rows past V read zeros (range check), their logits are masked
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
+    auto issue = [&](int t, char* slot) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
-            const int i = wave + 4 * k;
-            const int vr = min(t * kLLRows + 4 * (i & 7) + (lane >> 4), a.V - 1);
-            ll_piece(slot, i, a.w + int64_t(vr) * a.ldw, lane);
+            const int i = wave + G::kWaves * k;
+            ll_piece(slot, i, rw, (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2, lane);
         }
     };
     // The exponent offset of a token is FIXED for the whole split: the first tile's max (no
-    // online rescale of O — a rescale of the 192 accumulators in a branch made the compiler
-    // spill them, and a max that moves by < kLLOverflow leaves every term < e^60, in fp32 and
-    // bf16 range).  If some token's logits exceed its offset by more than that, the workgroup
-    // runs the split again with offset = the true max (never on realistic logits).
-    f32x16_t O[OB];
+    // online rescale of O — a rescale of the accumulators in a branch made the compiler spill
+    // them, and a max that moves by < kLLOverflow leaves every term < e^60, in fp32 and bf16
+    // range).  If some token's logits exceed its offset by more than that, the workgroup flags
+    // itself and records the true maxima; the RESTART launch reruns the flagged workgroups with
+    // offset = the true max (never on realistic logits; the others exit at once).  A second
+    // launch rather than a loop around this one: with the loop, hipcc no longer told the next
+    // tile's DMA apart from this tile's reads and waited for the DMA before every tile.
     float mfix = -INFINITY, mtrue = -INFINITY, lrun = 0.0f;
-    for (int pass = 0; pass < 2; ++pass) {
+    if (RESTART) {
+        int f = 0;
 #pragma unroll
-        for (int b = 0; b < OB; ++b) O[b] = f32x16_t{};
-        lrun = 0.0f;
-        bool bad = false;
-        if (t0 < t1) issue(t0, smem);
-        for (int t = t0; t < t1; ++t) {
-            char* slot = smem + ((t - t0) & 1) * kStage;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t
-            __builtin_amdgcn_s_barrier();  // ... every wave's; and every wave is done with tile t-1
-            if (t + 1 < t1) issue(t + 1, smem + ((t + 1 - t0) & 1) * kStage);
-            f32x16_t s = f32x16_t{};
-#pragma unroll
-            for (int ks = 0; ks < KH; ++ks)
-                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ll_row_frag(slot, lane, hh * HW + 16 * ks), hf[ks], s, 0, 0,
-                                                            0);
-            ll_pair_sum(s, xbuf, wave, lane);
-            // s[r] = logit(token c32, vocab t·32 + (r&3) + 8(r>>2) + 4hi)
-            const int vb = t * kLLRows + 4 * hi;
-            float mx = -INFINITY;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                if (vb + (r & 3) + 8 * (r >> 2) >= a.V) s[r] = -INFINITY;
-                mx = fmaxf(mx, s[r]);
-            }
-            const int64_t dy = y - int64_t(t) * kLLRows;
-            if (pass == 0 && hh == 0 && valid && dy >= 0 && dy < kLLRows && int((dy >> 2) & 1) == hi) {
-                const int rr = int((dy & 3) + 4 * (dy >> 3));
-                float xl = s[0];
-#pragma unroll
-                for (int r = 1; r < 16; ++r) xl = r == rr ? s[r] : xl;
-                a.xlab[tm] = xl;
-            }
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
-            mtrue = fmaxf(mtrue, mx);
-            if (pass == 0 && t == t0) mfix = mx;
-            bad = bad || mx > mfix + kLLOverflow;
-            const float nm = -mfix * kLog2e;
-            float p[16];
-            float ls = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                p[r] = exp2_fast(fmaf(s[r], kLog2e, nm));
-                ls += p[r];
-            }
-            lrun += ls;
-            const bf16x8_t pb0 = pack8(p), pb1 = pack8(p + 8);
-#pragma unroll
-            for (int b = 0; b < OB; ++b) {
-                const int dc = hh * HW + 32 * b;
-                O[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ll_tr_frag(slot, lane, 0, dc), pb0, O[b], 0, 0, 0);
-                O[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ll_tr_frag(slot, lane, 1, dc), pb1, O[b], 0, 0, 0);
-            }
-        }
-        if (!__syncthreads_or(bad)) break;
-        mfix = mtrue;  // every tile's max is now <= the offset
+        for (int w = 0; w < G::kWaves; ++w) f |= a.flags[blockIdx.x * G::kWaves + w];
+        if (!f) return;
+        mfix = a.mlpart[int64_t(split) * a.N + tc].x;  // the true max pass 0 found
     }
-    const float mrun = mfix;
+    f32x16_t O[OB];
+#pragma unroll
+    for (int b = 0; b < OB; ++b) O[b] = f32x16_t{};
+    bool bad = false;
+    if (t0 < t1) issue(t0, smem);
+    // one tile: the three LDS regions as __restrict__ parameters of an inlined call, so the
+    // compiler's alias scopes tell the next tile's DMA (nxt) apart from this tile's reads
+    // (cur, xb); without them it waited for that DMA before the first read of every tile
+    auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, char* __restrict__ xb, int t) __attribute__((always_inline)) {
+        if (t + 1 < t1) issue(t + 1, nxt);
+        f32x16_t s = ll_s_product<KS>(cur + sq * HS * 64, LL, hf);
+        ll_group_sum<G::NW>(s, xb, wave, lane);
+        // s[r] = logit(token c32, vocab t·32 + (r&3) + 8(r>>2) + 4hi)
+        const int vb = t * kLLRows + 4 * hi;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (vb + (r & 3) + 8 * (r >> 2) >= a.V) s[r] = -INFINITY;
+            mx = fmaxf(mx, s[r]);
+        }
+        const int64_t dy = y - int64_t(t) * kLLRows;
+        if (!RESTART && sq == 0 && valid && dy >= 0 && dy < kLLRows && int((dy >> 2) & 1) == hi) {
+            const int rr = int((dy & 3) + 4 * (dy >> 3));
+            float xl = s[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) xl = r == rr ? s[r] : xl;
+            a.xlab[tm] = xl;
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        if (!RESTART) {
+            mtrue = fmaxf(mtrue, mx);
+            if (t == t0) mfix = mx;
+            bad = bad || mx > mfix + kLLOverflow;
+        }
+        const float nm = -mfix * kLog2e;
+        float p[16];
+        float ls = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            p[r] = exp2_fast(fmaf(s[r], kLog2e, nm));
+            ls += p[r];
+        }
+        lrun += ls;
+        const bf16x8_t pb0 = pack8(p), pb1 = pack8(p + 8);
+        ll_tr_product<OB, false>(cur + sq * HS * 64, LL, pb0, pb1, O);
+    };
+    for (int t = t0; t < t1; ++t) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces of tile t
+        __builtin_amdgcn_s_barrier();  // ... every wave's; and every wave is done with tile t-1
+        tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, xbuf, t);
+    }
+    // the first launch flags an overflowed wave and records the true maxima as its m (its O / l
+    // are then discarded: the restart launch reruns the workgroup).  A flag word per wave: a
+    // workgroup-wide vote (__syncthreads_or) here brought back the per-tile DMA wait above.
+    bool any = false;
+    if (!RESTART) {
+        any = __any(bad);
+        if (lane == 0) a.flags[blockIdx.x * G::kWaves + wave] = any;
+    }
+    const float mrun = any ? mtrue : mfix;
     const float ltok = lrun + __shfl_xor(lrun, 32);
     if (valid) {
-        // O[b][r] = O(token c32, hidden hh·HW + 32b + (r&3) + 8(r>>2) + 4hi)
-        float* op = a.opart + (int64_t(split) * a.N + tm) * a.H + hh * HW + 4 * hi;
+        // O[b][r] = O(token c32, hidden sq·HS + 32b + (r&3) + 8(r>>2) + 4hi)
+        float* op = a.opart + (int64_t(split) * a.N + tm) * a.H + sq * HS + 4 * hi;
 #pragma unroll
         for (int b = 0; b < OB; ++b)
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 *reinterpret_cast<f32x4_t*>(op + 32 * b + 8 * q) =
                     f32x4_t{O[b][4 * q], O[b][4 * q + 1], O[b][4 * q + 2], O[b][4 * q + 3]};
-        if (hh == 0 && hi == 0) a.mlpart[int64_t(split) * a.N + tm] = make_float2(mrun, ltok);
+        if (sq == 0 && hi == 0) a.mlpart[int64_t(split) * a.N + tm] = make_float2(mrun, ltok);
     }
 }
 
@@ -407,80 +522,79 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
 }
 
 // ------------------------------------------------------------------ dW
-// Workgroup = 64 vocab rows (2 pairs x 32) x one token split; the W fragments stay in
+// Workgroup = NG·32 vocab rows x one token split; the W fragments of its rows stay in
 // registers, 32-token tiles of h (+ their lse / g / label) stream through LDS:
-//   S[t][v] = Σ_d h[t][d]·W[v][d]        (pair-summed over hidden halves, as in the forward)
+//   S[t][v] = Σ_d h[t][d]·W[v][d]        (group-summed over hidden slices, as in the forward)
 //   dS = g_t·(1[y_t = v] − 2^(S·log2e − lse_t·log2e))  -> bf16, the A operand of
-//   dW[v][d] += Σ_t dS[t][v]·h[t][d]     (12 d-blocks x 2 k-steps, h read transposed)
-template <int KH>
-__global__ __launch_bounds__(kLLThreads, 1) void k_lmloss_dw(LmLossArgs a) {
-    constexpr int HW = 16 * KH, H = 2 * HW, OB = HW / 32, NI = H / 64;
-    constexpr int kStage = kLLRows * H * 2 + 512;  // h tile + {-lse·log2e, g, y, y} x 32 tokens
-    __shared__ __attribute__((aligned(16))) char smem[2 * kStage + kLLXchg];
+//   dW[v][d] += Σ_t dS[t][v]·h[t][d]     (OB d-blocks x 2 k-steps, h read transposed)
+template <class G>
+__global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
+    constexpr int HS = G::HS, KS = G::KS, OB = G::OB, NI = G::NI, H = G::H;
+    constexpr int kStage = G::kStage + 512;  // h tile + {-lse·log2e, g, y, y} x 32 tokens
+    __shared__ __attribute__((aligned(16))) char smem[2 * kStage + G::kWaves * 4096];
     char* xbuf = smem + 2 * kStage;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, pr = wave >> 1, hh = wave & 1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave / G::NW, sq = wave % G::NW;
     const int hi = lane >> 5, c32 = lane & 31;
+    const LlLane LL = ll_lane(lane);
     const int nv = a.rows ? *a.nrows : a.N;
-    const int nvb = (a.V + kLLVocTile - 1) / kLLVocTile;
+    const int vpw = 32 * G::NG;
+    const int nvb = (a.V + vpw - 1) / vpw;
     const int vb = int(blockIdx.x) % nvb, ts = int(blockIdx.x) / nvb;
-    const int v0 = vb * kLLVocTile + pr * 32;
+    const int v0 = vb * vpw + grp * 32;
     const int ntt = (nv + kLLRows - 1) / kLLRows;
     const int t0 = int(int64_t(ts) * ntt / a.tsplit), t1 = int(int64_t(ts + 1) * ntt / a.tsplit);
-    bf16x8_t wf[KH];  // B operand of S: lane -> vocab row v0 + c32, hidden hh·HW + 16ks + 8hi + j
+    bf16x8_t wf[KS];  // B operand of S: lane -> vocab row v0 + c32, hidden sq·HS + 16ks + 8hi + j
     {
         const int vr = v0 + c32;
         if (vr < a.V) {
-            const uint16_t* wp = a.w + int64_t(vr) * a.ldw + hh * HW + 8 * hi;
+            const uint16_t* wp = a.w + int64_t(vr) * a.ldw + sq * HS + 8 * hi;
 #pragma unroll
-            for (int ks = 0; ks < KH; ++ks) wf[ks] = *reinterpret_cast<const bf16x8_t*>(wp + 16 * ks);
+            for (int ks = 0; ks < KS; ++ks) wf[ks] = *reinterpret_cast<const bf16x8_t*>(wp + 16 * ks);
         } else {
 #pragma unroll
-            for (int ks = 0; ks < KH; ++ks) wf[ks] = bf16x8_t{};
+            for (int ks = 0; ks < KS; ++ks) wf[ks] = bf16x8_t{};
         }
     }
-    // the two tile rows this lane's DMA pieces fetch (k even: r0, k odd: r0 + 16)
-    const int r0 = 4 * wave + (lane >> 4);
+    // the tile rows this lane's DMA pieces fetch: 4·(i & 7) + lane/16 for piece i = wave + kWaves·k
     auto tok_row = [&](int m) { const int mc = min(m, nv - 1); return a.rows ? a.rows[mc] : mc; };
     int rowA = 0, rowB = 0;
+    const int rA = ll_piece_row(wave, lane), rB = ll_piece_row(wave + G::kWaves, lane);
     if (t0 < t1) {
-        rowA = tok_row(t0 * kLLRows + r0);
-        rowB = tok_row(t0 * kLLRows + r0 + 16);
+        rowA = tok_row(t0 * kLLRows + rA);
+        rowB = tok_row(t0 * kLLRows + rB);
     }
-    auto issue = [&](int t, char* slot, int ra, int rb) {
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.h, uint32_t(int64_t(a.N) * a.ldh * 2));
+    const __amdgpu_buffer_rsrc_t rnl = make_rsrc(a.nlse, uint32_t(a.N) * 4u);
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gbuf, uint32_t(a.N) * 4u);
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.ybuf, uint32_t(a.N) * 4u);
+    auto issue = [&](int t, char* slot, int ra, int rb) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
-            const int i = wave + 4 * k;
-            ll_piece(slot, i, a.h + int64_t((k & 1) ? rb : ra) * a.ldh, lane);
+            const int i = wave + G::kWaves * k;
+            ll_piece(slot, i, rh, (((i & 7) == (wave & 7)) ? ra : rb) * int(a.ldh) * 2, lane);
         }
         if (wave == 0) {  // token scalars: lanes 0-31 -lse·log2e, 32-63 g; then the labels twice
             const int mi = min(t * kLLRows + c32, nv - 1);
-            const float* src = hi ? a.gbuf + mi : a.nlse + mi;
-            char* sc = slot + kLLRows * H * 2;
-            __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)sc, 4, 0, 0);
-            __builtin_amdgcn_global_load_lds(a.ybuf + mi, (__attribute__((address_space(3))) void*)(sc + 256), 4, 0, 0);
+            char* sc = slot + G::kStage;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(hi ? rg : rnl, (__attribute__((address_space(3))) void*)sc, 4,
+                                                     mi * 4, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (__attribute__((address_space(3))) void*)(sc + 256), 4, mi * 4,
+                                                     0, 0, 0);
         }
     };
     f32x16_t D[OB];
 #pragma unroll
     for (int b = 0; b < OB; ++b) D[b] = f32x16_t{};
     if (t0 < t1) issue(t0, smem, rowA, rowB);
-    for (int t = t0; t < t1; ++t) {
-        char* slot = smem + ((t - t0) & 1) * kStage;
-        if (t + 1 < t1) {  // next tile's row indices (their loads retire with this tile's pieces)
-            rowA = tok_row((t + 1) * kLLRows + r0);
-            rowB = tok_row((t + 1) * kLLRows + r0 + 16);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (t + 1 < t1) issue(t + 1, smem + ((t + 1 - t0) & 1) * kStage, rowA, rowB);
-        f32x16_t s = f32x16_t{};
-#pragma unroll
-        for (int ks = 0; ks < KH; ++ks)
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ll_row_frag(slot, lane, hh * HW + 16 * ks), wf[ks], s, 0, 0, 0);
-        ll_pair_sum(s, xbuf, wave, lane);
+    // one tile (as in the forward: restrict parameters give the DMA and the reads distinct
+    // alias scopes)
+    auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, char* __restrict__ xb, int t) __attribute__((always_inline)) {
+        if (t + 1 < t1) issue(t + 1, nxt, rowA, rowB);
+        f32x16_t s = ll_s_product<KS>(cur + sq * HS * 64, LL, wf);
+        ll_group_sum<G::NW>(s, xb, wave, lane);
         // s[r] = logit(token t·32 + (r&3) + 8(r>>2) + 4hi, vocab v0 + c32)
-        const float* scal = reinterpret_cast<const float*>(slot + kLLRows * H * 2);
-        const int* ys = reinterpret_cast<const int*>(slot + kLLRows * H * 2 + 256);
+        const float* scal = reinterpret_cast<const float*>(cur + G::kStage);
+        const int* ys = reinterpret_cast<const int*>(cur + G::kStage + 256);
         const int vcol = v0 + c32;
         float ds[16];
 #pragma unroll
@@ -501,20 +615,28 @@ __global__ __launch_bounds__(kLLThreads, 1) void k_lmloss_dw(LmLossArgs a) {
             }
         }
         const bf16x8_t db0 = pack8(ds), db1 = pack8(ds + 8);
-#pragma unroll
-        for (int b = 0; b < OB; ++b) {
-            const int dc = hh * HW + 32 * b;
-            D[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(db0, ll_tr_frag(slot, lane, 0, dc), D[b], 0, 0, 0);
-            D[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(db1, ll_tr_frag(slot, lane, 1, dc), D[b], 0, 0, 0);
+        ll_tr_product<OB, true>(cur + sq * HS * 64, LL, db0, db1, D);
+    };
+    for (int t = t0; t < t1; ++t) {
+        if (t + 1 < t1 && a.rows) {  // next tile's row indices (their loads retire with this tile's pieces)
+            rowA = tok_row((t + 1) * kLLRows + rA);
+            rowB = tok_row((t + 1) * kLLRows + rB);
+        } else if (t + 1 < t1) {
+            rowA = min((t + 1) * kLLRows + rA, nv - 1);
+            rowB = min((t + 1) * kLLRows + rB, nv - 1);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, xbuf, t);
     }
-    // D[b][r] = dW(vocab v0 + (r&3) + 8(r>>2) + 4hi, hidden hh·HW + 32b + c32)
+    (void)H;
+    // D[b][r] = dW(vocab v0 + (r&3) + 8(r>>2) + 4hi, hidden sq·HS + 32b + c32)
     const bool part = a.tsplit > 1;  // fp32 partials of this token split, summed by k_lmloss_dw_reduce
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int v = v0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
         if (v < a.V) {
-            const int64_t o = int64_t(v) * a.lddw + hh * HW + c32;
+            const int64_t o = int64_t(v) * a.lddw + sq * HS + c32;
             if (part || a.dw_dtype == TRLX_F32) {
                 float* out = static_cast<float*>(a.dw) + (part ? int64_t(ts) * a.V * a.lddw : 0) + o;
 #pragma unroll
@@ -625,6 +747,7 @@ struct LlWs {
     int* ybuf;
     int* order;
     int* cnt;
+    int* flags;
     float* dwpart;
 };
 // Workspace carve-up for N tokens (dwpart only when the dW kernel splits tokens).
@@ -645,6 +768,7 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, int tsplit, 
     t.ybuf = reinterpret_cast<int*>(take(size_t(N) * 4));
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t((N + kMaskChunk - 1) / kMaskChunk + 1) * 4));
+    t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 4 * 4));  // <= 4 waves per workgroup
     t.dwpart = reinterpret_cast<float*>(take(tsplit > 1 ? size_t(tsplit) * V * H * 4 : 0));
     if (w) *w = t;
     return off;
@@ -677,23 +801,28 @@ static int ll_check(const void* hidden, int64_t ldh, const void* weight, int64_t
     return TRLX_OK;
 }
 
-template <int KH>
+template <class G>
 static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
-    const int64_t ntt = (a.N + kLLTokTile - 1) / kLLTokTile;
-    hipLaunchKernelGGL(k_lmloss_fwd<KH>, dim3(unsigned(ntt * a.nsplit)), dim3(kLLThreads), 0, s, a);
-    return check_launch("k_lmloss_fwd");
+    const int64_t ntt = (a.N + 32 * G::NG - 1) / (32 * G::NG);
+    void (*first)(LmLossArgs) = k_lmloss_fwd<G, false>;
+    void (*restart)(LmLossArgs) = k_lmloss_fwd<G, true>;
+    hipLaunchKernelGGL(first, dim3(unsigned(ntt * a.nsplit)), dim3(G::kThreads), 0, s, a);
+    const int rc = check_launch("k_lmloss_fwd");
+    if (rc) return rc;
+    hipLaunchKernelGGL(restart, dim3(unsigned(ntt * a.nsplit)), dim3(G::kThreads), 0, s, a);
+    return check_launch("k_lmloss_fwd restart");
 }
-template <int KH>
+template <class G>
 static int ll_launch_dw(const LmLossArgs& a, hipStream_t s) {
-    const int64_t nvb = (a.V + kLLVocTile - 1) / kLLVocTile;
-    hipLaunchKernelGGL(k_lmloss_dw<KH>, dim3(unsigned(nvb * a.tsplit)), dim3(kLLThreads), 0, s, a);
+    const int64_t nvb = (a.V + 32 * G::NG - 1) / (32 * G::NG);
+    hipLaunchKernelGGL(k_lmloss_dw<G>, dim3(unsigned(nvb * a.tsplit)), dim3(G::kThreads), 0, s, a);
     return check_launch("k_lmloss_dw");
 }
 static int ll_fwd(const LmLossArgs& a, hipStream_t s) {
-    return a.H == 512 ? ll_launch_fwd<16>(a, s) : ll_launch_fwd<24>(a, s);
+    return a.H == 512 ? ll_launch_fwd<LlG512>(a, s) : ll_launch_fwd<LlG768>(a, s);
 }
 static int ll_dw(const LmLossArgs& a, hipStream_t s) {
-    return a.H == 512 ? ll_launch_dw<16>(a, s) : ll_launch_dw<24>(a, s);
+    return a.H == 512 ? ll_launch_dw<LlG512>(a, s) : ll_launch_dw<LlG768>(a, s);
 }
 
 // the common part: shapes, workspace, optional compaction from the mask
@@ -721,6 +850,7 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.nlse = w.nlse;
     a.gbuf = w.gbuf;
     a.ybuf = w.ybuf;
+    a.flags = w.flags;
     a.dw = a.tsplit > 1 ? static_cast<void*>(w.dwpart) : dweight;
     a.lddw = a.tsplit > 1 ? H : lddw;
     a.dw_dtype = dw_dtype;
