@@ -203,3 +203,36 @@ def test_loss_from_hidden_deterministic_and_drop_in():
     m = d["mask"].bool()
     assert _rel(hg.grad[m], outs[0][2][m]) < 5e-3 and _rel(wg.grad, outs[0][3]) < 5e-3
     torch.testing.assert_close(vg.grad, outs[0][4], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("splits,tsplit", [(1, 1), (3, 2), (8, 5), (5, 16)])
+def test_lm_head_logprobs_split_plans(splits, tsplit):
+    """Forced grid plans (tuning keys): the forward's vocab split count and the dW kernel's
+    token split of its last-round vocab blocks change only the fp32 summation order — every
+    plan stays within the fp64 tolerances, and matches the default plan to fp32 / bf16
+    rounding."""
+    N, H, V = 200, 768, 7000
+    h, w, y = _operands(N, H, V, 5)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(6))
+
+    def run():
+        hg = h.to(DEV).requires_grad_(True)
+        wg = w.to(DEV).requires_grad_(True)
+        lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32)
+        (lp * gout.to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+        return lp.detach(), hg.grad, wg.grad
+
+    base = run()
+    P._lib.set_tuning("lmloss_splits", splits)
+    P._lib.set_tuning("lmloss_dw_tsplit", tsplit)
+    try:
+        got = run()
+    finally:
+        P._lib.set_tuning("lmloss_splits", 0)
+        P._lib.set_tuning("lmloss_dw_tsplit", 0)
+    lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
+    torch.testing.assert_close(got[0].double(), lp64, rtol=1e-5, atol=2e-5)
+    assert _rel(got[1], dh64) < 1e-2 and _rel(got[2], dw64) < 1e-2
+    torch.testing.assert_close(got[0], base[0], rtol=1e-6, atol=1e-5)
+    assert _rel(got[1], base[1]) < 2e-3 and _rel(got[2], base[2]) < 2e-3

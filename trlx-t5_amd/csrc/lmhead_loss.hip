@@ -45,6 +45,7 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 constexpr int kLLRows = 32;            // rows of a staged tile: vocab rows (forward) / tokens (dW)
 constexpr int kLLMaxSplits = 8;        // vocab splits of the forward (workspace sizing)
+constexpr int kLLTokBlock = 64;        // tokens per forward workgroup (LlGeom: NG = 2 groups of 32)
 constexpr float kLLOverflow = 60.0f;   // logit - offset bound of the fixed-offset softmax (e^60)
 
 enum LmLossMode { kLLPpo = 0, kLLFwd = 1, kLLBwd = 2 };
@@ -60,10 +61,10 @@ struct LmLossArgs {
     // ones after them (k_mask_order); NULL = every token, row m
     const int* rows;
     const int* nrows;
-    int nsplit;
+    int nsplit;       // vocab splits of the forward: the maximum (nsplit_fixed: exactly)
+    int nsplit_fixed;
     float* opart;    // [nsplit][N][H] partial O (compact token index)
     float2* mlpart;  // [nsplit][N] partial (m, l)
-    float* xlab;     // [N] label logit (compact)
     float* nlse;     // [N] -lse·log2e (compact; read by the dW kernel)
     float* gbuf;     // [N] d loss / d lp (compact)
     int* ybuf;       // [N] label (compact)
@@ -77,10 +78,15 @@ struct LmLossArgs {
     void* dh;        // [N, lddh] d hidden (token rows)
     int64_t lddh;
     int dh_dtype;
-    void* dw;        // [V, lddw] d weight of dw_dtype (or [tsplit][V][H] fp32 partials)
+    void* dw;        // [V, lddw] d weight of dw_dtype
     int64_t lddw;
     int dw_dtype;
-    int tsplit;
+    // dW grid: dw_full workgroups own a vocab block each over all tokens; the remaining vocab
+    // blocks are split tsplit ways over the tokens into fp32 partials ([j][vpw][H]) that
+    // k_lmloss_dw_reduce sums in split order (the last, partial round of workgroups)
+    int dw_full, tsplit, dw_nblk;
+    float* dwpart;
+    int ncu;         // compute units (the forward's split choice, ll_fwd_splits)
     int mode;
     // ---- per-token PPO fields (the names ppo_token.h reads; see RowArgs in vocab_rows.hip)
     const void* old_lp;
@@ -180,13 +186,30 @@ __device__ __forceinline__ bf16x8_t pack8(const float* p) {
     return r;
 }
 
-// Scheduling masks of __builtin_amdgcn_sched_group_barrier (LLVM AMDGPU): MFMA, DS read.
-constexpr int kSgMfma = 0x008, kSgDsRead = 0x100;
+// Scheduling masks of __builtin_amdgcn_sched_group_barrier (LLVM AMDGPU): VALU, MFMA, any
+// VMEM (the LDS-DMA loads), DS read.
+constexpr int kSgValu = 0x002, kSgMfma = 0x008, kSgVmem = 0x010, kSgDsRead = 0x100;
+
+// s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt 7,
+// lgkmcnt 15): the builtin, unlike inline asm, is seen by the compiler's own wait insertion.
+constexpr int ll_vmcnt(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
+
+// max / sum of a value over lanes l and l^32 (one token's two halves), the same bits in both
+__device__ __forceinline__ float ll_pair_max(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float ll_pair_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 // S tile of one wave over its hidden slice: KS MFMAs whose streamed operand is read by rows.
-// Pipelined by sched groups: 3 reads ahead, then (1 MFMA, 1 read) pairs — left to itself the
-// compiler issued each read right before its MFMA and waited for it (LDS latency every step).
-template <int KS>
+// Pipelined by sched groups: 3 reads ahead, then (1 MFMA, 1 read, NV vector instructions)
+// per gap — left to itself the compiler issued each read right before its MFMA and waited for
+// it; NV > 0 pulls independent vector work of the same region (the previous tile's softmax)
+// into the MFMA gaps.
+template <int KS, int NV>
 __device__ __forceinline__ f32x16_t ll_s_product(const char* slice, const LlLane& L, const bf16x8_t* regs) {
     f32x16_t s = f32x16_t{};
     bf16x8_t af[KS];
@@ -199,14 +222,20 @@ __device__ __forceinline__ f32x16_t ll_s_product(const char* slice, const LlLane
     for (int k = 0; k < KS - 3; ++k) {
         __builtin_amdgcn_sched_group_barrier(kSgMfma, 1, 0);
         __builtin_amdgcn_sched_group_barrier(kSgDsRead, 1, 0);
+        if (NV) __builtin_amdgcn_sched_group_barrier(kSgValu, NV, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(kSgMfma, 3, 0);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        __builtin_amdgcn_sched_group_barrier(kSgMfma, 1, 0);
+        if (NV) __builtin_amdgcn_sched_group_barrier(kSgValu, NV, 0);
+    }
     return s;
 }
 // The second product over the wave's slice: OB blocks of 32 hidden columns x 2 k-steps, the
 // staged tile read transposed (4 reads per block); LEFT: the register operand is the A operand
-// (dW = dSᵀ·h), else the B operand (Oᵀ = Wᵀ·Pᵀ).  Pipelined one block ahead.
-template <int OB, bool LEFT>
+// (dW = dSᵀ·h), else the B operand (Oᵀ = Wᵀ·Pᵀ).  Pipelined one block ahead; NDMA > 0 spreads
+// that many LDS-DMA pieces of the region (the tile after next) over the MFMA gaps.
+template <int OB, bool LEFT, int NDMA>
 __device__ __forceinline__ void ll_tr_product(const char* slice, const LlLane& L, bf16x8_t r0, bf16x8_t r1,
                                               f32x16_t* acc) {
     bf16x8_t t[OB][2];
@@ -230,19 +259,30 @@ __device__ __forceinline__ void ll_tr_product(const char* slice, const LlLane& L
     for (int b = 0; b < OB - 2; ++b) {
         __builtin_amdgcn_sched_group_barrier(kSgMfma, 2, 0);
         __builtin_amdgcn_sched_group_barrier(kSgDsRead, 4, 0);
+        if (b < NDMA) __builtin_amdgcn_sched_group_barrier(kSgVmem, 1, 0);
     }
     __builtin_amdgcn_sched_group_barrier(kSgMfma, 4, 0);
+    constexpr int kRest = NDMA > OB - 2 ? NDMA - (OB - 2) : 0;
+    if (kRest) __builtin_amdgcn_sched_group_barrier(kSgVmem, kRest ? kRest : 1, 0);
 }
+
+// A workgroup barrier ordering LDS only.  __syncthreads() and an LDS-scope release fence both
+// wait for vmcnt(0) — the tile DMAs still in flight are LDS writes too — so the barrier is
+// spelled out: this wave's LDS accesses done, then s_barrier (the memory clobber keeps the
+// compiler from moving loads / stores across it).
+__device__ __forceinline__ void ll_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // The NW waves of a group add their partial S tiles (each over its slice of the hidden
 // dimension) through LDS, in the fixed order of their slice index, so every wave of the group
-// ends with the same bits.  Barrier inside: every wave of the workgroup must call it.
-template <int NW>
-__device__ __forceinline__ void ll_group_sum(f32x16_t& s, char* xbuf, int wave, int lane) {
+// ends with the same bits.  Write, a workgroup barrier (the caller's), read.
+__device__ __forceinline__ void ll_group_write(const f32x16_t& s, char* xbuf, int wave, int lane) {
     f32x4_t* mine = reinterpret_cast<f32x4_t*>(xbuf + wave * 4096);
 #pragma unroll
     for (int q = 0; q < 4; ++q) mine[q * 64 + lane] = f32x4_t{s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]};
-    __syncthreads();
+}
+template <int NW>
+__device__ __forceinline__ f32x16_t ll_group_read(const char* xbuf, int wave, int lane) {
+    f32x16_t s;
     const f32x4_t* o = reinterpret_cast<const f32x4_t*>(xbuf + (wave - wave % NW) * 4096);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // own slice read back too: nothing of s stays live across the barrier
@@ -252,8 +292,14 @@ __device__ __forceinline__ void ll_group_sum(f32x16_t& s, char* xbuf, int wave, 
 #pragma unroll
         for (int j = 1; j < NW; ++j) v[0] += v[j];
         s[4 * q] = v[0].x; s[4 * q + 1] = v[0].y; s[4 * q + 2] = v[0].z; s[4 * q + 3] = v[0].w;
-        __builtin_amdgcn_sched_barrier(0);  // 4 reads in flight at a time (registers)
     }
+    return s;
+}
+template <int NW>
+__device__ __forceinline__ void ll_group_sum(f32x16_t& s, char* xbuf, int wave, int lane) {
+    ll_group_write(s, xbuf, wave, lane);
+    ll_lds_barrier();
+    s = ll_group_read<NW>(xbuf, wave, lane);
 }
 
 // Workgroup geometry: NG groups of NW waves; a group owns 32 tokens (forward) / 32 vocab rows
@@ -267,6 +313,7 @@ struct LlGeom {
     static constexpr int kPieces = H / 16, NI = kPieces / kWaves;  // 1-KB DMA pieces per tile / per wave
     static constexpr int kStage = kLLRows * H * 2;
     static_assert(kPieces % kWaves == 0 && HS % 128 == 0, "geometry: slices start on 128-column segments");
+    static_assert(32 * NG == kLLTokBlock, "forward token block (ll_fwd_splits callers)");
     static_assert(kWaves <= 4, "forward overflow flags: 4 words per workgroup (ll_carve)");
 };
 // 4 waves (one per SIMD, 512 registers each): at H = 768 a wave holds 96 h / W fragment
@@ -275,32 +322,49 @@ struct LlGeom {
 typedef LlGeom<768, 2, 2> LlG768;
 typedef LlGeom<512, 2, 2> LlG512;
 
+// Vocab splits of the forward for ntb live token blocks: the count (<= a.nsplit) whose last
+// round of workgroups is fullest — cost = ceil(ntb·ns / ncu) / ns rounds of one whole-vocab
+// block; ties go to more splits.  A pure function of the device-side token count, so the
+// combine recomputes it.
+__device__ __forceinline__ int ll_fwd_splits(const LmLossArgs& a, int ntb) {
+    if (a.nsplit_fixed) return a.nsplit;
+    int best = 1;
+    float bc = 3.0e38f;
+    for (int ns = 1; ns <= a.nsplit; ++ns) {
+        const float c = float((ntb * ns + a.ncu - 1) / a.ncu) / float(ns);
+        if (c <= bc) {
+            bc = c;
+            best = ns;
+        }
+    }
+    return best;
+}
+
 // ------------------------------------------------------------------ forward (flash-O)
 // Workgroup = NG·32 tokens x one vocab split; wave (group g, slice q).  Per 32-row vocab tile:
 //   S^T[v][t] = Σ_d W[v][d]·h[t][d]   (KS MFMAs over the wave's hidden slice, group sum in LDS)
-//   P = exp(S - offset) per token (lanes t and t^32 hold its 32 values), Σ P, label logit
+//   P = exp(S - offset) per token (lanes t and t^32 hold its 32 values), Σ P
 //   O^T[d][t] += Σ_v W[v][d]·P[t][v] (OB d-blocks x 2 k-steps: W read transposed, P = the S
 //   accumulator converted to bf16 as the B operand): each lane's O registers are ONE token's.
-// 8 waves (2 per SIMD) at H = 768: 48 + 96 fragment / accumulator registers per wave leave the
-// compiler room to keep LDS reads in flight ahead of the MFMAs (a 4-wave, 2-slice layout at
-// 96 + 192 registers serialised every ds_read with its MFMA).
+// One wave per SIMD, so the softmax's vector work only overlaps matrix work of the SAME wave:
+// the loop is software-pipelined one tile deep — step t runs S(t+1)'s MFMAs with softmax(t)'s
+// vector instructions in their gaps (sched groups), then O(t)'s MFMAs with tile t+2's DMA in
+// theirs.  Three 48-KB stages (t, t+1 read; t+2 landing) + the 16-KB group-sum exchange = the
+// whole 160 KB.  The label logit is not picked here: k_lmloss_combine dots h with W[y].
 template <class G, bool RESTART>
-__global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
+__device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit, int nv) {
     constexpr int HS = G::HS, KS = G::KS, OB = G::OB, NI = G::NI, kStage = G::kStage;
-    __shared__ __attribute__((aligned(16))) char smem[2 * kStage + G::kWaves * 4096];
-    char* xbuf = smem + 2 * kStage;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave / G::NW, sq = wave % G::NW;
+    char* xbuf = smem + 3 * kStage;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), grp = wave / G::NW, sq = wave % G::NW;
     const int hi = lane >> 5, c32 = lane & 31;
     const LlLane LL = ll_lane(lane);
-    const int nv = a.rows ? *a.nrows : a.N;
-    const int split = int(blockIdx.x) % a.nsplit, mt = int(blockIdx.x) / a.nsplit;
+    const int split = lin / ntb, mt = lin - split * ntb;
     const int m0 = mt * 32 * G::NG;
-    if (m0 >= nv) return;  // past the compacted tokens (the grid's last blocks)
     const int tm = m0 + grp * 32 + c32;
     const bool valid = tm < nv;
     const int tc = valid ? tm : nv - 1;
     const int row = a.rows ? a.rows[tc] : tc;
-    const int64_t y = valid ? a.labels[int64_t(row) * a.lb] : -1;
     bf16x8_t hf[KS];  // B operand of S^T: lane -> token c32, hidden sq·HS + 16ks + 8hi + j
     {
         const uint16_t* hp = a.h + int64_t(row) * a.ldh + sq * HS + 8 * hi;
@@ -308,64 +372,51 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
         for (int ks = 0; ks < KS; ++ks) hf[ks] = *reinterpret_cast<const bf16x8_t*>(hp + 16 * ks);
     }
     const int nvt = (a.V + kLLRows - 1) / kLLRows;
-    const int t0 = int(int64_t(split) * nvt / a.nsplit), t1 = int(int64_t(split + 1) * nvt / a.nsplit);
-    // W rows by buffer loads: rows past V read zeros (range check), their logits are masked
+    const int t0 = int(int64_t(split) * nvt / nsplit), t1 = int(int64_t(split + 1) * nvt / nsplit);
+    // W rows by buffer loads: rows past V read zeros (range check), their logits are masked.
+    // A tile index past the split gives an out-of-range offset: the pieces fetch nothing.
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
     auto issue = [&](int t, char* slot) __attribute__((always_inline)) {
+        const bool live = t < t1;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             const int i = wave + G::kWaves * k;
-            ll_piece(slot, i, rw, (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2, lane);
+            const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
+            ll_piece(slot, i, rw, live ? off : int(0x7ffff000), lane);
         }
     };
     // The exponent offset of a token is FIXED for the whole split: the first tile's max (no
     // online rescale of O — a rescale of the accumulators in a branch made the compiler spill
     // them, and a max that moves by < kLLOverflow leaves every term < e^60, in fp32 and bf16
-    // range).  If some token's logits exceed its offset by more than that, the workgroup flags
+    // range).  If some token's logits exceed its offset by more than that, the wave flags
     // itself and records the true maxima; the RESTART launch reruns the flagged workgroups with
     // offset = the true max (never on realistic logits; the others exit at once).  A second
     // launch rather than a loop around this one: with the loop, hipcc no longer told the next
     // tile's DMA apart from this tile's reads and waited for the DMA before every tile.
     float mfix = -INFINITY, mtrue = -INFINITY, lrun = 0.0f;
-    if (RESTART) {
-        int f = 0;
-#pragma unroll
-        for (int w = 0; w < G::kWaves; ++w) f |= a.flags[blockIdx.x * G::kWaves + w];
-        if (!f) return;
-        mfix = a.mlpart[int64_t(split) * a.N + tc].x;  // the true max pass 0 found
-    }
+    if (RESTART) mfix = a.mlpart[int64_t(split) * a.N + tc].x;  // the true max pass 0 found
     f32x16_t O[OB];
 #pragma unroll
     for (int b = 0; b < OB; ++b) O[b] = f32x16_t{};
     bool bad = false;
-    if (t0 < t1) issue(t0, smem);
-    // one tile: the three LDS regions as __restrict__ parameters of an inlined call, so the
-    // compiler's alias scopes tell the next tile's DMA (nxt) apart from this tile's reads
-    // (cur, xb); without them it waited for that DMA before the first read of every tile
-    auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, char* __restrict__ xb, int t) __attribute__((always_inline)) {
-        if (t + 1 < t1) issue(t + 1, nxt);
-        f32x16_t s = ll_s_product<KS>(cur + sq * HS * 64, LL, hf);
-        ll_group_sum<G::NW>(s, xb, wave, lane);
-        // s[r] = logit(token c32, vocab t·32 + (r&3) + 8(r>>2) + 4hi)
-        const int vb = t * kLLRows + 4 * hi;
+    // softmax of tile t's summed S (s[r] = logit(token c32, vocab t·32 + (r&3) + 8(r>>2) + 4hi)):
+    // branch-free so it shares a scheduling region with the next tile's MFMAs
+    // (only the vocab's last tile can be partial: it is the last split's last tile, whose
+    // softmax runs after the loop — MASK there only)
+    auto softmax = [&](f32x16_t s, int t, bf16x8_t& pb0, bf16x8_t& pb1, auto mask_tag) __attribute__((always_inline)) {
+        constexpr bool MASK = decltype(mask_tag)::value;
         float mx = -INFINITY;
+        if (MASK) {
+            const int lim = a.V - t * kLLRows - 4 * hi;  // rows with (r&3) + 8(r>>2) < lim exist
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (vb + (r & 3) + 8 * (r >> 2) >= a.V) s[r] = -INFINITY;
-            mx = fmaxf(mx, s[r]);
+            for (int r = 0; r < 16; ++r) s[r] = (r & 3) + 8 * (r >> 2) < lim ? s[r] : -INFINITY;
         }
-        const int64_t dy = y - int64_t(t) * kLLRows;
-        if (!RESTART && sq == 0 && valid && dy >= 0 && dy < kLLRows && int((dy >> 2) & 1) == hi) {
-            const int rr = int((dy & 3) + 4 * (dy >> 3));
-            float xl = s[0];
 #pragma unroll
-            for (int r = 1; r < 16; ++r) xl = r == rr ? s[r] : xl;
-            a.xlab[tm] = xl;
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
+        mx = ll_pair_max(mx);
         if (!RESTART) {
             mtrue = fmaxf(mtrue, mx);
-            if (t == t0) mfix = mx;
+            mfix = t == t0 ? mx : mfix;
             bad = bad || mx > mfix + kLLOverflow;
         }
         const float nm = -mfix * kLog2e;
@@ -377,24 +428,58 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
             ls += p[r];
         }
         lrun += ls;
-        const bf16x8_t pb0 = pack8(p), pb1 = pack8(p + 8);
-        ll_tr_product<OB, false>(cur + sq * HS * 64, LL, pb0, pb1, O);
+        pb0 = pack8(p);
+        pb1 = pack8(p + 8);
     };
-    for (int t = t0; t < t1; ++t) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces of tile t
-        __builtin_amdgcn_s_barrier();  // ... every wave's; and every wave is done with tile t-1
-        tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, xbuf, t);
+    // step t (t + 1 < t1): the four LDS regions as __restrict__ parameters of an inlined call,
+    // so the compiler's alias scopes tell tile t+2's DMA (fut) apart from this step's reads
+    f32x16_t s;  // summed S of the tile whose softmax comes next
+    auto step = [&](const char* __restrict__ cur, const char* __restrict__ nx, char* __restrict__ fut,
+                    char* __restrict__ xb, int t) __attribute__((always_inline)) {
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t+1
+        ll_lds_barrier();  // every wave's; every wave is done with xb and with tile t-1
+        bf16x8_t pb0, pb1;
+        f32x16_t s1 = ll_s_product<KS, 5>(nx + sq * HS * 64, LL, hf);
+        softmax(s, t, pb0, pb1, std::false_type{});
+        ll_group_write(s1, xb, wave, lane);
+        issue(t + 2, fut);
+        ll_tr_product<OB, false, NI>(cur + sq * HS * 64, LL, pb0, pb1, O);
+        ll_lds_barrier();
+        s = ll_group_read<G::NW>(xb, wave, lane);
+    };
+    if (t0 < t1) {
+        char* c0 = smem;
+        char* c1 = smem + kStage;
+        char* c2 = smem + 2 * kStage;
+        issue(t0, c0);
+        issue(t0 + 1, c1);
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI));  // tile t0 (t0+1 may fly)
+        ll_lds_barrier();
+        s = ll_s_product<KS, 0>(c0 + sq * HS * 64, LL, hf);
+        ll_group_write(s, xbuf, wave, lane);
+        ll_lds_barrier();
+        s = ll_group_read<G::NW>(xbuf, wave, lane);
+        for (int t = t0; t + 1 < t1; ++t) {
+            step(c0, c1, c2, xbuf, t);
+            char* c = c0;
+            c0 = c1;
+            c1 = c2;
+            c2 = c;
+        }
+        bf16x8_t pb0, pb1;  // the last tile: its softmax and O product
+        softmax(s, t1 - 1, pb0, pb1, std::true_type{});
+        ll_tr_product<OB, false, 0>(c0 + sq * HS * 64, LL, pb0, pb1, O);
     }
     // the first launch flags an overflowed wave and records the true maxima as its m (its O / l
     // are then discarded: the restart launch reruns the workgroup).  A flag word per wave: a
-    // workgroup-wide vote (__syncthreads_or) here brought back the per-tile DMA wait above.
+    // workgroup-wide vote (__syncthreads_or) here brought back a per-tile DMA wait.
     bool any = false;
     if (!RESTART) {
         any = __any(bad);
-        if (lane == 0) a.flags[blockIdx.x * G::kWaves + wave] = any;
+        if (lane == 0) a.flags[lin * G::kWaves + wave] = any;
     }
     const float mrun = any ? mtrue : mfix;
-    const float ltok = lrun + __shfl_xor(lrun, 32);
+    const float ltok = ll_pair_sum(lrun);
     if (valid) {
         // O[b][r] = O(token c32, hidden sq·HS + 32b + (r&3) + 8(r>>2) + 4hi)
         float* op = a.opart + (int64_t(split) * a.N + tm) * a.H + sq * HS + 4 * hi;
@@ -405,6 +490,35 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
                 *reinterpret_cast<f32x4_t*>(op + 32 * b + 8 * q) =
                     f32x4_t{O[b][4 * q], O[b][4 * q + 1], O[b][4 * q + 2], O[b][4 * q + 3]};
         if (sq == 0 && hi == 0) a.mlpart[int64_t(split) * a.N + tm] = make_float2(mrun, ltok);
+    }
+}
+
+// The first launch: one (token block, split) per workgroup; the split count follows the live
+// token count (ll_fwd_splits), and each XCD (blockIdx % 8) takes a contiguous run of the
+// split-major order, so the workgroups sharing an L2 stream the same W rows.  The RESTART
+// launch (one workgroup per CU) walks the blocks and reruns the flagged ones.
+template <class G, bool RESTART>
+__global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * G::kStage + G::kWaves * 4096];
+    static_assert(3 * G::kStage + G::kWaves * 4096 <= 163840, "forward LDS: 3 stages + exchange");
+    const int nv = a.rows ? *a.nrows : a.N;
+    const int ntb = (nv + 32 * G::NG - 1) / (32 * G::NG);
+    const int nsplit = ll_fwd_splits(a, ntb);
+    const int total = ntb * nsplit;
+    if (!RESTART) {
+        const int per_xcd = (total + 7) / 8;
+        const int kx = int(blockIdx.x) >> 3, lin = (int(blockIdx.x) & 7) * per_xcd + kx;
+        if (kx >= per_xcd || lin >= total) return;  // past an XCD's share / the live tokens
+        ll_fwd_block<G, false>(a, smem, lin, ntb, nsplit, nv);
+        return;
+    }
+    for (int lin = int(blockIdx.x); lin < total; lin += int(gridDim.x)) {
+        int f = 0;
+#pragma unroll
+        for (int w = 0; w < G::kWaves; ++w) f |= a.flags[lin * G::kWaves + w];
+        if (!f) continue;
+        ll_fwd_block<G, true>(a, smem, lin, ntb, nsplit, nv);
+        ll_lds_barrier();  // every wave is done with the LDS before the next block reuses it
     }
 }
 
@@ -443,12 +557,33 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
     }
     const int64_t y = a.labels[int64_t(row) * a.lb];
     const bool yok = y >= 0 && y < a.V;
+    const uint16_t* wrow = a.w + (yok ? y : 0) * a.ldw;
     float lse = 0.0f, L = 1.0f;
+    int nsplit = 0;
     if (MODE != kLLBwd) {
+        // the label logit h·W[y] (fp32 products of the bf16 operands, fixed-order sums), kept
+        // out of the forward's tile loop
+        float xl = 0.0f;
+        const uint16_t* hrow = a.h + int64_t(row) * a.ldh;
+        for (int d4 = tid; d4 < H4; d4 += blockDim.x) {
+            const uint2 hv = reinterpret_cast<const uint2*>(hrow)[d4];
+            const uint2 wv = reinterpret_cast<const uint2*>(wrow)[d4];
+            xl = fmaf(bf_lo(hv.x), bf_lo(wv.x), xl);
+            xl = fmaf(bf_hi(hv.x), bf_hi(wv.x), xl);
+            xl = fmaf(bf_lo(hv.y), bf_lo(wv.y), xl);
+            xl = fmaf(bf_hi(hv.y), bf_hi(wv.y), xl);
+        }
+        for (int off = 32; off > 0; off >>= 1) xl += __shfl_xor(xl, off);
+        if ((tid & 63) == 0) s_tok[tid >> 6] = xl;
+        __syncthreads();
+        const float xlab = (s_tok[0] + s_tok[1]) + (s_tok[2] + s_tok[3]);
+        __syncthreads();  // s_tok is reused below
         float M = -INFINITY;
-        for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.mlpart[int64_t(s) * a.N + m].x);
+        const int nv = a.rows ? *a.nrows : a.N;
+        nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
+        for (int s = 0; s < nsplit; ++s) M = fmaxf(M, a.mlpart[int64_t(s) * a.N + m].x);
         L = 0.0f;
-        for (int s = 0; s < a.nsplit; ++s) {
+        for (int s = 0; s < nsplit; ++s) {
             const float2 p = a.mlpart[int64_t(s) * a.N + m];
             const float sc = p.x == -INFINITY ? 0.0f : exp2_fast((p.x - M) * kLog2e);
             L += p.y * sc;
@@ -457,7 +592,7 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
         const float lsum = logf(L);
         lse = M + lsum;
         if (tid == 0) {
-            const float lp = yok ? (a.xlab[m] - M) - lsum : NAN;  // the reference's order, as in the rows
+            const float lp = yok ? (xlab - M) - lsum : NAN;  // the reference's order, as in the rows
             float g = 0.0f;
             if (MODE == kLLPpo) {
                 float vin[3];
@@ -491,14 +626,13 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
     __syncthreads();
     const float g = s_tok[0];
     const float invL = 1.0f / L;
-    const uint16_t* wrow = a.w + (yok ? y : 0) * a.ldw;
     for (int d4 = tid; d4 < H4; d4 += blockDim.x) {
         f32x4_t e;
         if (MODE == kLLBwd) {
             e = reinterpret_cast<const f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4];
         } else {
             e = f32x4_t{};
-            for (int s = 0; s < a.nsplit; ++s)
+            for (int s = 0; s < nsplit; ++s)
                 e += s_sc[s] * reinterpret_cast<const f32x4_t*>(a.opart + (int64_t(s) * a.N + m) * a.H)[d4];
             e *= invL;
         }
@@ -538,11 +672,14 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
     const LlLane LL = ll_lane(lane);
     const int nv = a.rows ? *a.nrows : a.N;
     const int vpw = 32 * G::NG;
-    const int nvb = (a.V + vpw - 1) / vpw;
-    const int vb = int(blockIdx.x) % nvb, ts = int(blockIdx.x) / nvb;
+    // a whole vocab block over every token, or (the last round) a token split of one
+    const bool part = int(blockIdx.x) >= a.dw_full;
+    const int j = int(blockIdx.x) - a.dw_full;
+    const int vb = part ? a.dw_full + j / a.tsplit : int(blockIdx.x);
+    const int ts = part ? j % a.tsplit : 0, nts = part ? a.tsplit : 1;
     const int v0 = vb * vpw + grp * 32;
     const int ntt = (nv + kLLRows - 1) / kLLRows;
-    const int t0 = int(int64_t(ts) * ntt / a.tsplit), t1 = int(int64_t(ts + 1) * ntt / a.tsplit);
+    const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
     bf16x8_t wf[KS];  // B operand of S: lane -> vocab row v0 + c32, hidden sq·HS + 16ks + 8hi + j
     {
         const int vr = v0 + c32;
@@ -590,7 +727,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
     // alias scopes)
     auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, char* __restrict__ xb, int t) __attribute__((always_inline)) {
         if (t + 1 < t1) issue(t + 1, nxt, rowA, rowB);
-        f32x16_t s = ll_s_product<KS>(cur + sq * HS * 64, LL, wf);
+        f32x16_t s = ll_s_product<KS, 0>(cur + sq * HS * 64, LL, wf);
         ll_group_sum<G::NW>(s, xb, wave, lane);
         // s[r] = logit(token t·32 + (r&3) + 8(r>>2) + 4hi, vocab v0 + c32)
         const float* scal = reinterpret_cast<const float*>(cur + G::kStage);
@@ -615,7 +752,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
             }
         }
         const bf16x8_t db0 = pack8(ds), db1 = pack8(ds + 8);
-        ll_tr_product<OB, true>(cur + sq * HS * 64, LL, db0, db1, D);
+        ll_tr_product<OB, true, 0>(cur + sq * HS * 64, LL, db0, db1, D);
     };
     for (int t = t0; t < t1; ++t) {
         if (t + 1 < t1 && a.rows) {  // next tile's row indices (their loads retire with this tile's pieces)
@@ -625,20 +762,22 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
             rowA = min((t + 1) * kLLRows + rA, nv - 1);
             rowB = min((t + 1) * kLLRows + rB, nv - 1);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t
+        ll_lds_barrier();  // every wave's; and every wave is done with tile t-1
         tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, xbuf, t);
     }
-    (void)H;
     // D[b][r] = dW(vocab v0 + (r&3) + 8(r>>2) + 4hi, hidden sq·HS + 32b + c32)
-    const bool part = a.tsplit > 1;  // fp32 partials of this token split, summed by k_lmloss_dw_reduce
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int v = v0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-        if (v < a.V) {
+        const int vr = grp * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi, v = vb * vpw + vr;
+        if (part) {  // fp32 partial of this token split, summed by k_lmloss_dw_reduce
+            float* out = a.dwpart + (int64_t(j) * vpw + vr) * H + sq * HS + c32;
+#pragma unroll
+            for (int b = 0; b < OB; ++b) out[32 * b] = D[b][r];
+        } else if (v < a.V) {
             const int64_t o = int64_t(v) * a.lddw + sq * HS + c32;
-            if (part || a.dw_dtype == TRLX_F32) {
-                float* out = static_cast<float*>(a.dw) + (part ? int64_t(ts) * a.V * a.lddw : 0) + o;
+            if (a.dw_dtype == TRLX_F32) {
+                float* out = static_cast<float*>(a.dw) + o;
 #pragma unroll
                 for (int b = 0; b < OB; ++b) out[32 * b] = D[b][r];
             } else {
@@ -650,13 +789,18 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
     }
 }
 
-// Fixed-order sum of the token-split dW partials: dw[v][d] = Σ_ts part[ts][v][d].
-__global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int tsplit, int64_t n, void* dw,
-                                                          int dw_dtype, int V, int H, int64_t lddw) {
+// Fixed-order sum of the token-split dW partials of the vocab blocks past dw_full:
+// dw[v][d] = Σ_ts part[b·tsplit + ts][r][d] for v = (dw_full + b)·vpw + r.
+__global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int tsplit, int nblk, int dw_full,
+                                                          int vpw, void* dw, int dw_dtype, int V, int H,
+                                                          int64_t lddw) {
+    const int64_t per = int64_t(vpw) * H, n = nblk * per;
     for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-        const int64_t v = i / H, d = i - v * H;
+        const int64_t b = i / per, e = i - b * per, r = e / H, d = e - r * H;
+        const int64_t v = (dw_full + b) * vpw + r;
+        if (v >= V) continue;
         float acc = 0.0f;
-        for (int s = 0; s < tsplit; ++s) acc += part[int64_t(s) * V * H + i];
+        for (int s = 0; s < tsplit; ++s) acc += part[(b * tsplit + s) * per + e];
         st_any(dw, dw_dtype, v * lddw + d, acc);
     }
 }
@@ -730,7 +874,7 @@ int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
         TRLX_REQUIRE(value >= 0 && value <= kLLMaxSplits, TRLX_ERR_ARG, "lmloss_splits: 0..%d", kLLMaxSplits);
         g_ll_splits = int(value);
     } else if (ts) {
-        TRLX_REQUIRE(value >= 0 && value <= 4, TRLX_ERR_ARG, "lmloss_dw_tsplit: 0..4");
+        TRLX_REQUIRE(value >= 0 && value <= 16, TRLX_ERR_ARG, "lmloss_dw_tsplit: 0..16");
         g_ll_tsplit = int(value);
     }
     return TRLX_OK;
@@ -741,7 +885,6 @@ static size_t ll_align(size_t x) { return (x + 255) & ~size_t(255); }
 struct LlWs {
     float* opart;
     float2* mlpart;
-    float* xlab;
     float* nlse;
     float* gbuf;
     int* ybuf;
@@ -750,8 +893,42 @@ struct LlWs {
     int* flags;
     float* dwpart;
 };
-// Workspace carve-up for N tokens (dwpart only when the dW kernel splits tokens).
-static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, int tsplit, LlWs* w) {
+// Compute units of the current device (the grid plans below).
+static int ll_ncu() {
+    static thread_local int dev = -1, ncu = 0;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return 256;
+    if (d != dev) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
+        dev = d;
+        ncu = n;
+    }
+    return ncu;
+}
+
+// dW grid plan: whole rounds of workgroups own a vocab block each; the blocks of the last,
+// partial round are split over the tokens so that round is (nearly) full instead of a tail of
+// a few long workgroups (C2: 786 blocks on 256 CUs = 3 rounds + 18 blocks, the 18 split 14 ways).
+struct LlDwPlan {
+    int full, tsplit, nblk;  // workgroups = full + nblk·tsplit
+};
+static LlDwPlan ll_dw_plan(int64_t V) {
+    const int ncu = ll_ncu();
+    const int nvb = int((V + kLLTokBlock - 1) / kLLTokBlock);
+    const int rem = nvb % ncu;
+    LlDwPlan p{nvb, 1, 0};
+    if (g_ll_tsplit == 1 || rem == 0) return p;
+    const int ts = g_ll_tsplit ? g_ll_tsplit : std::min(16, ncu / rem);
+    if (ts <= 1) return p;
+    p.full = nvb - rem;
+    p.tsplit = ts;
+    p.nblk = rem;
+    return p;
+}
+
+// Workspace carve-up for N tokens (dwpart: the split blocks' fp32 partials).
+static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w) {
     char* p = static_cast<char*>(base);
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -762,28 +939,16 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, int tsplit, 
     LlWs t;
     t.opart = reinterpret_cast<float*>(take(size_t(kLLMaxSplits) * N * H * 4));
     t.mlpart = reinterpret_cast<float2*>(take(size_t(kLLMaxSplits) * N * 8));
-    t.xlab = reinterpret_cast<float*>(take(size_t(N) * 4));
     t.nlse = reinterpret_cast<float*>(take(size_t(N) * 4));
     t.gbuf = reinterpret_cast<float*>(take(size_t(N) * 4));
     t.ybuf = reinterpret_cast<int*>(take(size_t(N) * 4));
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t((N + kMaskChunk - 1) / kMaskChunk + 1) * 4));
     t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 4 * 4));  // <= 4 waves per workgroup
-    t.dwpart = reinterpret_cast<float*>(take(tsplit > 1 ? size_t(tsplit) * V * H * 4 : 0));
+    const LlDwPlan dp = ll_dw_plan(V);
+    t.dwpart = reinterpret_cast<float*>(take(size_t(dp.nblk) * dp.tsplit * kLLTokBlock * H * 4));
     if (w) *w = t;
     return off;
-}
-
-static int ll_tsplit(int64_t V) {
-    if (g_ll_tsplit) return g_ll_tsplit;
-    (void)V;
-    return 1;
-}
-
-static int ll_splits(int64_t N) {
-    if (g_ll_splits) return g_ll_splits;
-    (void)N;
-    return kLLMaxSplits;
 }
 
 static int ll_check(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N, int64_t H,
@@ -801,21 +966,23 @@ static int ll_check(const void* hidden, int64_t ldh, const void* weight, int64_t
     return TRLX_OK;
 }
 
+// The forward's grid covers the largest split plan (every token live, a.nsplit splits),
+// rounded up to whole XCD shares; each workgroup finds its (token block, split) on the device.
 template <class G>
 static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
-    const int64_t ntt = (a.N + 32 * G::NG - 1) / (32 * G::NG);
+    const int64_t ntb = (a.N + kLLTokBlock - 1) / kLLTokBlock;
+    const unsigned grid = unsigned((ntb * a.nsplit + 7) / 8 * 8);
     void (*first)(LmLossArgs) = k_lmloss_fwd<G, false>;
     void (*restart)(LmLossArgs) = k_lmloss_fwd<G, true>;
-    hipLaunchKernelGGL(first, dim3(unsigned(ntt * a.nsplit)), dim3(G::kThreads), 0, s, a);
+    hipLaunchKernelGGL(first, dim3(grid), dim3(G::kThreads), 0, s, a);
     const int rc = check_launch("k_lmloss_fwd");
     if (rc) return rc;
-    hipLaunchKernelGGL(restart, dim3(unsigned(ntt * a.nsplit)), dim3(G::kThreads), 0, s, a);
+    hipLaunchKernelGGL(restart, dim3(unsigned(std::min<int64_t>(grid, a.ncu))), dim3(G::kThreads), 0, s, a);
     return check_launch("k_lmloss_fwd restart");
 }
 template <class G>
 static int ll_launch_dw(const LmLossArgs& a, hipStream_t s) {
-    const int64_t nvb = (a.V + 32 * G::NG - 1) / (32 * G::NG);
-    hipLaunchKernelGGL(k_lmloss_dw<G>, dim3(unsigned(nvb * a.tsplit)), dim3(G::kThreads), 0, s, a);
+    hipLaunchKernelGGL(k_lmloss_dw<G>, dim3(unsigned(a.dw_full + a.dw_nblk * a.tsplit)), dim3(G::kThreads), 0, s, a);
     return check_launch("k_lmloss_dw");
 }
 static int ll_fwd(const LmLossArgs& a, hipStream_t s) {
@@ -841,18 +1008,23 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.V = int(V);
     a.labels = labels;
     a.lb = lb;
-    a.nsplit = ll_splits(N);
-    a.tsplit = ll_tsplit(V);
-    ll_carve(lm_ws, N, H, V, a.tsplit, &w);
+    a.nsplit = g_ll_splits ? g_ll_splits : kLLMaxSplits;
+    a.nsplit_fixed = g_ll_splits != 0;
+    a.ncu = ll_ncu();
+    const LlDwPlan dp = ll_dw_plan(V);
+    a.dw_full = dp.full;
+    a.tsplit = dp.tsplit;
+    a.dw_nblk = dp.nblk;
+    ll_carve(lm_ws, N, H, V, &w);
+    a.dwpart = w.dwpart;
     a.opart = w.opart;
     a.mlpart = w.mlpart;
-    a.xlab = w.xlab;
     a.nlse = w.nlse;
     a.gbuf = w.gbuf;
     a.ybuf = w.ybuf;
     a.flags = w.flags;
-    a.dw = a.tsplit > 1 ? static_cast<void*>(w.dwpart) : dweight;
-    a.lddw = a.tsplit > 1 ? H : lddw;
+    a.dw = dweight;
+    a.lddw = lddw;
     a.dw_dtype = dw_dtype;
     if (compact_mask) {
         const int nchunk = int((N + kMaskChunk - 1) / kMaskChunk);
@@ -871,10 +1043,9 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
 static int ll_dw_finish(const LmLossArgs& a, void* dweight, int dw_dtype, int64_t lddw, const LlWs& w,
                         hipStream_t s) {
     int rc = ll_dw(a, s);
-    if (rc || a.tsplit <= 1) return rc;
-    const int64_t n = int64_t(a.V) * a.H;
-    hipLaunchKernelGGL(k_lmloss_dw_reduce, dim3(2048), dim3(256), 0, s, w.dwpart, a.tsplit, n, dweight, dw_dtype, a.V,
-                       a.H, lddw);
+    if (rc || a.dw_nblk == 0) return rc;
+    hipLaunchKernelGGL(k_lmloss_dw_reduce, dim3(1024), dim3(256), 0, s, w.dwpart, a.tsplit, a.dw_nblk, a.dw_full,
+                       kLLTokBlock, dweight, dw_dtype, a.V, a.H, lddw);
     return check_launch("k_lmloss_dw_reduce");
 }
 
@@ -883,7 +1054,7 @@ static int ll_dw_finish(const LmLossArgs& a, void* dweight, int dw_dtype, int64_
 using namespace trlx;
 
 extern "C" int64_t trlx_lmhead_loss_workspace_bytes(int64_t N, int64_t H, int64_t V) {
-    return int64_t(ll_carve(nullptr, N, H, V, ll_tsplit(V), nullptr));
+    return int64_t(ll_carve(nullptr, N, H, V, nullptr));
 }
 
 extern "C" int trlx_ppo_loss_from_hidden(
