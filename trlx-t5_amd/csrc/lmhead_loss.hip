@@ -46,7 +46,33 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 constexpr int kLLRows = 32;            // rows of a staged tile: vocab rows (forward) / tokens (dW)
 constexpr int kLLMaxSplits = 8;        // vocab splits of the forward (workspace sizing)
 constexpr int kLLTokBlock = 64;        // tokens per forward workgroup (LlGeom: NG = 2 groups of 32)
-constexpr float kLLOverflow = 60.0f;   // logit - offset bound of the fixed-offset softmax (e^60)
+constexpr float kLLOverflow = 60.0f;
+// Diagnostic builds only (-DLL_ABLATE=bits, never the shipped library): drop parts of the
+// forward's steady-state step to price them — 1 softmax, 2 group-sum exchange, 4 next DMA,
+// 8 O product, 16 S product.  Results are wrong in such a build.
+#ifndef LL_ABLATE
+#define LL_ABLATE 0
+#endif
+constexpr int kLLAblate = LL_ABLATE;
+
+// Diagnostic builds only (-DLL_STAMP=1): s_memtime segment sums of the forward's step per wave
+// in g_ll_stamps (read by trlx_debug_ll_stamps); no stamp executes in the shipped library.
+#ifndef LL_STAMP
+#define LL_STAMP 0
+#endif
+#if LL_STAMP
+__device__ unsigned long long g_ll_stamps[1 << 16];
+#define LL_TS(v)                                                                              \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");             \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+    } while (0)
+#else
+#define LL_TS(v) \
+    do {         \
+    } while (0)
+#endif   // logit - offset bound of the fixed-offset softmax (e^60)
 
 enum LmLossMode { kLLPpo = 0, kLLFwd = 1, kLLBwd = 2 };
 
@@ -134,11 +160,15 @@ __device__ __forceinline__ int ll_piece_row(int i, int lane) { return 8 * ((i & 
 // of the lane's row in the resource): hipcc then tracks these LDS writes like the s2 lm_head
 // kernel's and does not put a vmcnt(0) in front of the next LDS read (the flat
 // global_load_lds form made every tile wait for the DMA of the NEXT one before its first read).
-__device__ __forceinline__ void ll_piece(char* slot, int i, __amdgpu_buffer_rsrc_t rs, int row_bytes, int lane) {
+// The byte offset in the row-major source of the 16 B that lane `lane` of piece i carries.
+__device__ __forceinline__ int ll_piece_src(int i, int row_bytes, int lane) {
     const int r = ll_piece_row(i, lane);
     const int ch = 4 * (2 * (i & 1) + (lane >> 5)) + ((lane & 3) ^ ((r >> 2) & 3));
+    return row_bytes + (i >> 3) * 256 + ch * 16;
+}
+__device__ __forceinline__ void ll_piece(char* slot, int i, __amdgpu_buffer_rsrc_t rs, int row_bytes, int lane) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
-                                             row_bytes + (i >> 3) * 256 + ch * 16, 0, 0, 0);
+                                             ll_piece_src(i, row_bytes, lane), 0, 0, 0);
 }
 
 // Per-lane byte offsets of the two operand reads inside a staged tile, for a wave whose hidden
@@ -433,19 +463,132 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
     };
     // step t (t + 1 < t1): the four LDS regions as __restrict__ parameters of an inlined call,
     // so the compiler's alias scopes tell tile t+2's DMA (fut) apart from this step's reads
+    // One DMA piece k (of NI) of tile t into slot (an out-of-range offset past the split).
+    auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
+        const int i = wave + G::kWaves * k;
+        const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
+        ll_piece(slot, i, rw, t < t1 ? off : int(0x7ffff000), lane);
+    };
+    // The step's schedule is written out gap by gap, each gap fenced (sched_barrier): the
+    // compiler's own interleave left the softmax's vector work and the DMA issue in segments of
+    // their own (stamps: 1529 cycles for S + softmax, 678 for the exchange write + 12 DMA issues,
+    // against 768 of MFMA each side).
+    //   S phase, gap k (KS gaps): row read k+4 | MFMA k of S(t+1) | softmax(t) chunk k
+    //   O phase, gap i (2·OB gaps, k-step-major): tr read i+4 | MFMA i of O(t) | P's second half
+    //     packed (i = 0), S(t+1)'s partial written (i = 2..5), at i = OB the exchange barrier and
+    //     the partner's partial read (summed after the loop, consumed by the next step)
+    //   and every 3rd gap from the step's start one LDS-DMA piece of tile t+2 (the last ones early
+    //   in the O phase, so they land before the next step's wait): a piece is 1 KB through the
+    //   CU's vector-memory path, and bunched pieces stall their wave's issue (stamps: 12 in a row
+    //   cost ~600 cycles)
     f32x16_t s;  // summed S of the tile whose softmax comes next
+#if LL_STAMP
+    unsigned long long stamp[8] = {};
+#endif
     auto step = [&](const char* __restrict__ cur, const char* __restrict__ nx, char* __restrict__ fut,
                     char* __restrict__ xb, int t) __attribute__((always_inline)) {
+        unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, ts5 = 0, ts6 = 0;
+        LL_TS(ts0);
         __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t+1
         ll_lds_barrier();  // every wave's; every wave is done with xb and with tile t-1
-        bf16x8_t pb0, pb1;
-        f32x16_t s1 = ll_s_product<KS, 5>(nx + sq * HS * 64, LL, hf);
-        softmax(s, t, pb0, pb1, std::false_type{});
-        ll_group_write(s1, xb, wave, lane);
-        issue(t + 2, fut);
-        ll_tr_product<OB, false, NI>(cur + sq * HS * 64, LL, pb0, pb1, O);
-        ll_lds_barrier();
-        s = ll_group_read<G::NW>(xb, wave, lane);
+        LL_TS(ts1);
+        // ---- S phase
+        const char* ns = nx + sq * HS * 64;
+        constexpr int PF = 4;
+        bf16x8_t af[KS];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) af[k] = ll_row_frag(ns, LL, k);
+        f32x16_t s1 = f32x16_t{};
+        float m0, m1, m2, m3, m4, m5, mx = 0.0f, nm = 0.0f, ls = 0.0f;
+        float p[16];
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            if (k + PF < KS) af[k + PF] = ll_row_frag(ns, LL, k + PF);
+            s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k], hf[k], s1, 0, 0, 0);
+            if (k == 0) {
+                m0 = fmaxf(fmaxf(s[0], s[1]), s[2]);
+                m1 = fmaxf(fmaxf(s[3], s[4]), s[5]);
+            } else if (k == 1) {
+                m2 = fmaxf(fmaxf(s[6], s[7]), s[8]);
+                m3 = fmaxf(fmaxf(s[9], s[10]), s[11]);
+            } else if (k == 2) {
+                m4 = fmaxf(fmaxf(s[12], s[13]), s[14]);
+                m5 = fmaxf(fmaxf(m0, m1), s[15]);
+            } else if (k == 3) {
+                mx = fmaxf(fmaxf(fmaxf(m2, m3), m4), m5);
+            } else if (k == 4) {
+                mx = ll_pair_max(mx);
+                if (!RESTART) {
+                    mtrue = fmaxf(mtrue, mx);
+                    mfix = t == t0 ? mx : mfix;
+                    bad = bad || mx > mfix + kLLOverflow;
+                }
+                nm = -mfix * kLog2e;
+            } else {
+                const int rlo = (k - 5) * 16 / (KS - 5), rhi = (k - 4) * 16 / (KS - 5);
+#pragma unroll
+                for (int r = rlo; r < rhi; ++r) {
+                    p[r] = exp2_fast(fmaf(s[r], kLog2e, nm));
+                    ls += p[r];
+                }
+            }
+            if (k % 3 == 1 && k / 3 < NI && !(kLLAblate & 4)) issue_piece(t + 2, fut, k / 3);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lrun += ls;
+        const bf16x8_t pb0 = pack8(p);
+        bf16x8_t pb1;
+        LL_TS(ts2);
+        LL_TS(ts3);
+        // ---- O phase
+        const char* cs = cur + sq * HS * 64;
+        constexpr int PFO = 4;
+        bf16x8_t tf[2 * OB];
+#pragma unroll
+        for (int i = 0; i < PFO; ++i) tf[i] = ll_tr_frag(cs, LL, i / OB, i % OB);
+        f32x4_t xv[4][G::NW];
+#pragma unroll
+        for (int i = 0; i < 2 * OB; ++i) {
+            if (i + PFO < 2 * OB) tf[i + PFO] = ll_tr_frag(cs, LL, (i + PFO) / OB, (i + PFO) % OB);
+            if (i == 0) pb1 = pack8(p + 8);
+            const int b = i % OB;
+            O[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[i], i < OB ? pb0 : pb1, O[b], 0, 0, 0);
+            if (i >= 2 && i < 6) {  // S(t+1)'s partial: quarter i-2
+                const int q = i - 2;
+                reinterpret_cast<f32x4_t*>(xb + wave * 4096)[q * 64 + lane] =
+                    f32x4_t{s1[4 * q], s1[4 * q + 1], s1[4 * q + 2], s1[4 * q + 3]};
+            }
+            if ((KS + i) % 3 == 1 && (KS + i) / 3 < NI && !(kLLAblate & 4)) issue_piece(t + 2, fut, (KS + i) / 3);
+            if (i == OB) {
+                LL_TS(ts4);
+                ll_lds_barrier();  // every wave's partial written
+                LL_TS(ts5);
+                const f32x4_t* o = reinterpret_cast<const f32x4_t*>(xb + (wave - wave % G::NW) * 4096);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int j = 0; j < G::NW; ++j) xv[q][j] = o[j * 256 + q * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4_t v = xv[q][0];
+#pragma unroll
+            for (int j = 1; j < G::NW; ++j) v += xv[q][j];
+            s[4 * q] = v.x; s[4 * q + 1] = v.y; s[4 * q + 2] = v.z; s[4 * q + 3] = v.w;
+        }
+        LL_TS(ts6);
+#if LL_STAMP
+        stamp[0] += ts1 - ts0;
+        stamp[1] += ts2 - ts1;
+        stamp[2] += ts3 - ts2;
+        stamp[3] += ts4 - ts3;
+        stamp[4] += ts5 - ts4;
+        stamp[5] += ts6 - ts5;
+        stamp[6] += 1;
+#endif
+        (void)ts0, (void)ts1, (void)ts2, (void)ts3, (void)ts4, (void)ts5, (void)ts6;
     };
     if (t0 < t1) {
         char* c0 = smem;
@@ -473,6 +616,10 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
     // the first launch flags an overflowed wave and records the true maxima as its m (its O / l
     // are then discarded: the restart launch reruns the workgroup).  A flag word per wave: a
     // workgroup-wide vote (__syncthreads_or) here brought back a per-tile DMA wait.
+#if LL_STAMP
+    if (lane == 0 && !RESTART && lin * G::kWaves + wave < (1 << 13))
+        for (int k = 0; k < 8; ++k) g_ll_stamps[(lin * G::kWaves + wave) * 8 + k] = stamp[k];
+#endif
     bool any = false;
     if (!RESTART) {
         any = __any(bad);
@@ -664,10 +811,11 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
 template <class G>
 __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
     constexpr int HS = G::HS, KS = G::KS, OB = G::OB, NI = G::NI, H = G::H;
-    constexpr int kStage = G::kStage + 512;  // h tile + {-lse·log2e, g, y, y} x 32 tokens
+    constexpr int kStage = G::kStage + 768;  // h tile + {-lse·log2e, g, y} x 64 lanes
     __shared__ __attribute__((aligned(16))) char smem[2 * kStage + G::kWaves * 4096];
     char* xbuf = smem + 2 * kStage;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = wave / G::NW, sq = wave % G::NW;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), grp = wave / G::NW, sq = wave % G::NW;
     const int hi = lane >> 5, c32 = lane & 31;
     const LlLane LL = ll_lane(lane);
     const int nv = a.rows ? *a.nrows : a.N;
@@ -692,76 +840,112 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
             for (int ks = 0; ks < KS; ++ks) wf[ks] = bf16x8_t{};
         }
     }
-    // the tile rows this lane's DMA pieces fetch: 4·(i & 7) + lane/16 for piece i = wave + kWaves·k
+    // the tile rows this lane's DMA pieces fetch (pieces i = wave + kWaves·k: two distinct rows),
+    // as byte offsets into h; with compaction the row indices are loaded a tile ahead
     auto tok_row = [&](int m) { const int mc = min(m, nv - 1); return a.rows ? a.rows[mc] : mc; };
-    int rowA = 0, rowB = 0;
     const int rA = ll_piece_row(wave, lane), rB = ll_piece_row(wave + G::kWaves, lane);
+    int rowA = 0, rowB = 0, nrowA = 0, nrowB = 0;
     if (t0 < t1) {
         rowA = tok_row(t0 * kLLRows + rA);
         rowB = tok_row(t0 * kLLRows + rB);
+        nrowA = tok_row((t0 + 1) * kLLRows + rA);
+        nrowB = tok_row((t0 + 1) * kLLRows + rB);
     }
     const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.h, uint32_t(int64_t(a.N) * a.ldh * 2));
     const __amdgpu_buffer_rsrc_t rnl = make_rsrc(a.nlse, uint32_t(a.N) * 4u);
     const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gbuf, uint32_t(a.N) * 4u);
     const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.ybuf, uint32_t(a.N) * 4u);
-    auto issue = [&](int t, char* slot, int ra, int rb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            const int i = wave + G::kWaves * k;
-            ll_piece(slot, i, rh, (((i & 7) == (wave & 7)) ? ra : rb) * int(a.ldh) * 2, lane);
-        }
-        if (wave == 0) {  // token scalars: lanes 0-31 -lse·log2e, 32-63 g; then the labels twice
-            const int mi = min(t * kLLRows + c32, nv - 1);
-            char* sc = slot + G::kStage;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(hi ? rg : rnl, (__attribute__((address_space(3))) void*)sc, 4,
-                                                     mi * 4, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (__attribute__((address_space(3))) void*)(sc + 256), 4, mi * 4,
-                                                     0, 0, 0);
-        }
+    // DMA piece k of tile t (rows ra / rb) into slot; a tile past the split fetches nothing
+    auto issue_piece = [&](int t, char* slot, int k, int ra, int rb) __attribute__((always_inline)) {
+        const int i = wave + G::kWaves * k;
+        const int off = ll_piece_src(i, (((i & 7) == (wave & 7)) ? ra : rb) * int(a.ldh) * 2, lane);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
+                                                 t < t1 ? off : int(0x7ffff000), 0, 0, 0);
+    };
+    // token scalars of tile t (wave 0): {-lse·log2e, g, y} of token min(t·32 + c32, nv-1) in
+    // lanes c32 and c32+32 alike
+    auto issue_scalars = [&](int t, char* slot) __attribute__((always_inline)) {
+        const int mi = (t < t1 ? min(t * kLLRows + c32, nv - 1) : 0x1fffffff) * 4;
+        char* sc = slot + G::kStage;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rnl, (__attribute__((address_space(3))) void*)sc, 4, mi, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (__attribute__((address_space(3))) void*)(sc + 256), 4, mi, 0, 0,
+                                                 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (__attribute__((address_space(3))) void*)(sc + 512), 4, mi, 0, 0,
+                                                 0);
     };
     f32x16_t D[OB];
 #pragma unroll
     for (int b = 0; b < OB; ++b) D[b] = f32x16_t{};
-    if (t0 < t1) issue(t0, smem, rowA, rowB);
-    // one tile (as in the forward: restrict parameters give the DMA and the reads distinct
-    // alias scopes)
+    if (t0 < t1) {
+#pragma unroll
+        for (int k = 0; k < NI; ++k) issue_piece(t0, smem, k, rowA, rowB);
+        if (wave == 0) issue_scalars(t0, smem);
+    }
+    const int vcol = v0 + c32;
+    // One tile, its schedule written out gap by gap (sched_barrier fences, as the forward's step):
+    //   S phase, gap k: row read k+4 | MFMA k of S(t) | every 3rd gap one DMA piece of tile t+1
+    //   exchange: the partial S written, barrier, the group's partials read and summed
+    //   dS of the tile's first 16 tokens (k-step 0) from S and the staged scalars
+    //   dW phase, gap i (k-step-major): tr read i+4 | dS of token half 2 (gaps 0-7, one value a
+    //     gap, packed at gap 7 for the k-step-1 MFMAs from gap OB) | MFMA i | DMA pieces left
     auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, char* __restrict__ xb, int t) __attribute__((always_inline)) {
-        if (t + 1 < t1) issue(t + 1, nxt, rowA, rowB);
-        f32x16_t s = ll_s_product<KS, 0>(cur + sq * HS * 64, LL, wf);
-        ll_group_sum<G::NW>(s, xb, wave, lane);
+        const int pa = nrowA, pb = nrowB;  // tile t+1's rows (loaded a tile ago)
+        if (a.rows) {  // tile t+2's rows for the next call: their loads retire during this tile
+            nrowA = tok_row((t + 2) * kLLRows + rA);
+            nrowB = tok_row((t + 2) * kLLRows + rB);
+        } else {
+            nrowA = min((t + 2) * kLLRows + rA, nv - 1);
+            nrowB = min((t + 2) * kLLRows + rB, nv - 1);
+        }
+        const char* hs = cur + sq * HS * 64;
+        constexpr int PF = 4;
+        bf16x8_t af[KS];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) af[k] = ll_row_frag(hs, LL, k);
+        f32x16_t s = f32x16_t{};
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            if (k + PF < KS) af[k + PF] = ll_row_frag(hs, LL, k + PF);
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k], wf[k], s, 0, 0, 0);
+            if (k % 3 == 1 && k / 3 < NI) issue_piece(t + 1, nxt, k / 3, pa, pb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (wave == 0) issue_scalars(t + 1, nxt);
+        ll_group_write(s, xb, wave, lane);
+        ll_lds_barrier();
+        s = ll_group_read<G::NW>(xb, wave, lane);
         // s[r] = logit(token t·32 + (r&3) + 8(r>>2) + 4hi, vocab v0 + c32)
         const float* scal = reinterpret_cast<const float*>(cur + G::kStage);
-        const int* ys = reinterpret_cast<const int*>(cur + G::kStage + 256);
-        const int vcol = v0 + c32;
+        const int* ys = reinterpret_cast<const int*>(cur + G::kStage + 512);
         float ds[16];
+        auto dsv = [&](int r) __attribute__((always_inline)) {
+            const int tb = 8 * (r >> 2) + 4 * hi + (r & 3);  // token of the tile
+            const float gv = t * kLLRows + tb < nv ? scal[64 + tb] : 0.0f;
+            const float pv = exp2_fast(fmaf(s[r], kLog2e, scal[tb]));
+            ds[r] = gv * ((ys[tb] == vcol ? 1.0f : 0.0f) - pv);
+        };
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int tb = 8 * q + 4 * hi;  // tokens tb .. tb+3 of the tile
-            const f32x4_t nl = *reinterpret_cast<const f32x4_t*>(scal + tb);
-            const f32x4_t gg = *reinterpret_cast<const f32x4_t*>(scal + 32 + tb);
-            const int4 yy = *reinterpret_cast<const int4*>(ys + tb);
-            const float nla[4] = {nl.x, nl.y, nl.z, nl.w}, ga[4] = {gg.x, gg.y, gg.z, gg.w};
-            const int ya[4] = {yy.x, yy.y, yy.z, yy.w};
+        for (int r = 0; r < 8; ++r) dsv(r);
+        const bf16x8_t db0 = pack8(ds);
+        bf16x8_t db1;
+        __builtin_amdgcn_sched_barrier(0);
+        const char* ts_ = cur + sq * HS * 64;
+        constexpr int PFO = 4;
+        bf16x8_t tf[2 * OB];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = 4 * q + e;
-                const bool tok_ok = t * kLLRows + tb + e < nv;
-                const float gv = tok_ok ? ga[e] : 0.0f;
-                const float pv = exp2_fast(fmaf(s[r], kLog2e, nla[e]));
-                ds[r] = gv * ((ya[e] == vcol ? 1.0f : 0.0f) - pv);
-            }
+        for (int i = 0; i < PFO; ++i) tf[i] = ll_tr_frag(ts_, LL, i / OB, i % OB);
+#pragma unroll
+        for (int i = 0; i < 2 * OB; ++i) {
+            if (i + PFO < 2 * OB) tf[i + PFO] = ll_tr_frag(ts_, LL, (i + PFO) / OB, (i + PFO) % OB);
+            if (i < 8) dsv(8 + i);
+            if (i == 7) db1 = pack8(ds + 8);  // before the first k-step-1 MFMA (gap OB >= 8)
+            const int b = i % OB;
+            D[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i < OB ? db0 : db1, tf[i], D[b], 0, 0, 0);
+            if ((KS + i) % 3 == 1 && (KS + i) / 3 < NI) issue_piece(t + 1, nxt, (KS + i) / 3, pa, pb);
+            __builtin_amdgcn_sched_barrier(0);
         }
-        const bf16x8_t db0 = pack8(ds), db1 = pack8(ds + 8);
-        ll_tr_product<OB, true, 0>(cur + sq * HS * 64, LL, db0, db1, D);
     };
     for (int t = t0; t < t1; ++t) {
-        if (t + 1 < t1 && a.rows) {  // next tile's row indices (their loads retire with this tile's pieces)
-            rowA = tok_row((t + 1) * kLLRows + rA);
-            rowB = tok_row((t + 1) * kLLRows + rB);
-        } else if (t + 1 < t1) {
-            rowA = min((t + 1) * kLLRows + rA, nv - 1);
-            rowB = min((t + 1) * kLLRows + rB, nv - 1);
-        }
         __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t
         ll_lds_barrier();  // every wave's; and every wave is done with tile t-1
         tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, xbuf, t);
@@ -1165,3 +1349,9 @@ extern "C" int trlx_lmhead_logprobs_bwd(const void* hidden, int64_t ldh, const v
     if (rc) return rc;
     return ll_dw_finish(a, dweight, dw_dtype, lddw, w, s);
 }
+
+#if LL_STAMP
+extern "C" int trlx_debug_ll_stamps(void* dst, int64_t n) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_ll_stamps), size_t(n) * 8) == hipSuccess ? 0 : 1;
+}
+#endif
