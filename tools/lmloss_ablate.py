@@ -54,11 +54,19 @@ def child(N, H, V, iters):
         import numpy as np
         fwd()
         torch.cuda.synchronize()
-        buf = np.zeros((1 << 13) * 8, dtype=np.uint64)
+        bwd()
+        torch.cuda.synchronize()
+        buf = np.zeros(1 << 16, dtype=np.uint64)
         lib = L.load()
         lib.trlx_debug_ll_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         assert lib.trlx_debug_ll_stamps(buf.ctypes.data, buf.size) == 0
-        sm = buf.reshape(-1, 8)
+        dm = buf[1 << 15:].reshape(-1, 8)
+        dm = dm[dm[:, 6] > 0].astype(np.float64)
+        if dm.size:
+            dper = dm[:, :5] / dm[:, 6:7]
+            out["dw_stamp_cycles_per_step"] = {n: round(float(v), 1) for n, v in zip(
+                ["wait_dma+barrier", "S_phase", "exchange", "dS_half", "dW_phase"], dper.mean(0))}
+        sm = buf[:1 << 15].reshape(-1, 8)
         sm = sm[sm[:, 6] > 0].astype(np.float64)
         per = sm[:, :6] / sm[:, 6:7]
         names = ["wait_dma+barrier", "S+softmax", "xwrite+dma_issue", "O_product", "mid_barrier", "xread"]

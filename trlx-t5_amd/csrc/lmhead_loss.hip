@@ -903,26 +903,53 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
 #pragma unroll
         for (int k = 0; k < PF; ++k) af[k] = ll_row_frag(hs, LL, k);
         f32x16_t s = f32x16_t{};
+        // this tile's token scalars into registers during the S phase (12 b128 reads of the
+        // staged {-lse·log2e, g, y}: tokens 8q + 4hi .. +3 for q = 0..3)
+        const char* scb = cur + G::kStage;
+        f32x4_t snl[4], sgg[4];
+        int4 syy[4];
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
             if (k + PF < KS) af[k + PF] = ll_row_frag(hs, LL, k + PF);
             s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k], wf[k], s, 0, 0, 0);
             if (k % 3 == 1 && k / 3 < NI) issue_piece(t + 1, nxt, k / 3, pa, pb);
+            if (k >= KS - 12) {
+                const int q = (k - (KS - 12)) & 3, tb = 8 * q + 4 * hi;
+                const int which = (k - (KS - 12)) >> 2;
+                if (which == 0) snl[q] = *reinterpret_cast<const f32x4_t*>(scb + 4 * tb);
+                else if (which == 1) sgg[q] = *reinterpret_cast<const f32x4_t*>(scb + 256 + 4 * tb);
+                else syy[q] = *reinterpret_cast<const int4*>(scb + 512 + 4 * tb);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
         if (wave == 0) issue_scalars(t + 1, nxt);
         ll_group_write(s, xb, wave, lane);
         ll_lds_barrier();
-        s = ll_group_read<G::NW>(xb, wave, lane);
+        // the group's partials, all read now; the first half summed here, the second half in the
+        // first dW gap (its reads land behind the first half's dS)
+        f32x4_t xv[4][G::NW];
+        {
+            const f32x4_t* o = reinterpret_cast<const f32x4_t*>(xb + (wave - wave % G::NW) * 4096);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int jj = 0; jj < G::NW; ++jj) xv[q][jj] = o[jj * 256 + q * 64 + lane];
+        }
+        auto xsum = [&](int q) __attribute__((always_inline)) {
+            f32x4_t v = xv[q][0];
+#pragma unroll
+            for (int jj = 1; jj < G::NW; ++jj) v += xv[q][jj];
+            s[4 * q] = v.x; s[4 * q + 1] = v.y; s[4 * q + 2] = v.z; s[4 * q + 3] = v.w;
+        };
+        xsum(0);
+        xsum(1);
         // s[r] = logit(token t·32 + (r&3) + 8(r>>2) + 4hi, vocab v0 + c32)
-        const float* scal = reinterpret_cast<const float*>(cur + G::kStage);
-        const int* ys = reinterpret_cast<const int*>(cur + G::kStage + 512);
         float ds[16];
         auto dsv = [&](int r) __attribute__((always_inline)) {
-            const int tb = 8 * (r >> 2) + 4 * hi + (r & 3);  // token of the tile
-            const float gv = t * kLLRows + tb < nv ? scal[64 + tb] : 0.0f;
-            const float pv = exp2_fast(fmaf(s[r], kLog2e, scal[tb]));
-            ds[r] = gv * ((ys[tb] == vcol ? 1.0f : 0.0f) - pv);
+            const int q = r >> 2, e = r & 3, tb = 8 * q + 4 * hi + e;  // token of the tile
+            const float gv = t * kLLRows + tb < nv ? sgg[q][e] : 0.0f;
+            const float pv = exp2_fast(fmaf(s[r], kLog2e, snl[q][e]));
+            ds[r] = gv * ((syy[q][e] == vcol ? 1.0f : 0.0f) - pv);
         };
 #pragma unroll
         for (int r = 0; r < 8; ++r) dsv(r);
@@ -937,6 +964,10 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
 #pragma unroll
         for (int i = 0; i < 2 * OB; ++i) {
             if (i + PFO < 2 * OB) tf[i + PFO] = ll_tr_frag(ts_, LL, (i + PFO) / OB, (i + PFO) % OB);
+            if (i == 0) {
+                xsum(2);
+                xsum(3);
+            }
             if (i < 8) dsv(8 + i);
             if (i == 7) db1 = pack8(ds + 8);  // before the first k-step-1 MFMA (gap OB >= 8)
             const int b = i % OB;
