@@ -670,7 +670,8 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
 }
 
 // ------------------------------------------------------------------ combine
-// One workgroup per compact token m: merge the vocab splits (fixed order), lse, lp, g, dh.
+// One workgroup per compact token m, one thread per 4 hidden columns (H/4 threads: 192 / 128):
+// merge the vocab splits (fixed order), lse, lp, g, dh.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
     const int m = blockIdx.x, tid = threadIdx.x;
@@ -723,7 +724,8 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
         for (int off = 32; off > 0; off >>= 1) xl += __shfl_xor(xl, off);
         if ((tid & 63) == 0) s_tok[tid >> 6] = xl;
         __syncthreads();
-        const float xlab = (s_tok[0] + s_tok[1]) + (s_tok[2] + s_tok[3]);
+        float xlab = s_tok[0];  // the waves' sums in wave order
+        for (int w = 1; w < int(blockDim.x >> 6); ++w) xlab += s_tok[w];
         __syncthreads();  // s_tok is reused below
         float M = -INFINITY;
         const int nv = a.rows ? *a.nrows : a.N;
@@ -1009,14 +1011,16 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
 __global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int tsplit, int nblk, int dw_full,
                                                           int vpw, void* dw, int dw_dtype, int V, int H,
                                                           int64_t lddw) {
-    const int64_t per = int64_t(vpw) * H, n = nblk * per;
-    for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-        const int64_t b = i / per, e = i - b * per, r = e / H, d = e - r * H;
+    const int64_t per4 = int64_t(vpw) * H / 4, n4 = nblk * per4;  // 4 columns a thread (H % 4 == 0)
+    for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n4; i += int64_t(gridDim.x) * blockDim.x) {
+        const int64_t b = i / per4, e = i - b * per4, r = (4 * e) / H, d = 4 * e - r * H;
         const int64_t v = (dw_full + b) * vpw + r;
         if (v >= V) continue;
-        float acc = 0.0f;
-        for (int s = 0; s < tsplit; ++s) acc += part[(b * tsplit + s) * per + e];
-        st_any(dw, dw_dtype, v * lddw + d, acc);
+        const f32x4_t* src = reinterpret_cast<const f32x4_t*>(part) + b * tsplit * per4 + e;
+        f32x4_t acc = src[0];
+        for (int s = 1; s < tsplit; ++s) acc += src[s * per4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st_any(dw, dw_dtype, v * lddw + d + c, acc[c]);
     }
 }
 
@@ -1320,7 +1324,7 @@ extern "C" int trlx_ppo_loss_from_hidden(
     a.dh_dtype = dh_dtype;
     rc = ll_fwd(a, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_lmloss_combine<kLLPpo>, dim3(unsigned(N)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_lmloss_combine<kLLPpo>, dim3(unsigned(N)), dim3(unsigned(H / 4)), 0, s, a);
     rc = check_launch("k_lmloss_combine");
     if (rc) return rc;
     return ll_dw_finish(a, dweight, dw_dtype, lddw, w, s);
@@ -1346,7 +1350,7 @@ extern "C" int trlx_lmhead_logprobs_fwd_saved(const void* hidden, int64_t ldh, c
     a.ebuf = e_out;
     rc = ll_fwd(a, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_lmloss_combine<kLLFwd>, dim3(unsigned(N)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_lmloss_combine<kLLFwd>, dim3(unsigned(N)), dim3(unsigned(H / 4)), 0, s, a);
     return check_launch("k_lmloss_combine");
 }
 
@@ -1375,7 +1379,7 @@ extern "C" int trlx_lmhead_logprobs_bwd(const void* hidden, int64_t ldh, const v
     a.dh = dhidden;
     a.lddh = lddh;
     a.dh_dtype = dh_dtype;
-    hipLaunchKernelGGL(k_lmloss_combine<kLLBwd>, dim3(unsigned(N)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_lmloss_combine<kLLBwd>, dim3(unsigned(N)), dim3(unsigned(H / 4)), 0, s, a);
     rc = check_launch("k_lmloss_combine");
     if (rc) return rc;
     return ll_dw_finish(a, dweight, dw_dtype, lddw, w, s);
