@@ -75,6 +75,11 @@ const char* trlx_last_error(void);
  *                       1 = all in VGPRs, 2 = 5 VGPR + 3 LDS vector steps, 3 = 6 + 2 (8 waves/SIMD)
  *   "ragged_order"      ragged experience rows with an order scratch: 0 = valid rows first (default),
  *                       1 = natural order
+ *   "order_launch"      the valid-rows-first order: 0 auto (one launch up to 64 chunks of 1024 rows,
+ *                       then two), 1 = one launch, 2 = two chunk-count launches
+ *   "lmloss_splits"     fused loss forward vocab splits: 0 auto (the fullest last round), 1..8 fixed
+ *   "lmloss_dw_tsplit"  fused loss dW: 0 auto (the last round's vocab blocks split over the tokens),
+ *                       1 = no split, 2..16 = that many token splits
  *   "store_policy"      gradient-row store cache policy: 0 auto (default: nt; sc1 for all-VGPR rows
  *                       launches writing > 1.5 GB), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
  * Results are identical up to fp32 summation order; only speed changes. */

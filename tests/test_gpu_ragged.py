@@ -263,13 +263,23 @@ def test_fused_abi_ragged_step():
     assert int(x["lengths"].sum()) < B * Tn  # a ragged batch
 
 
+@pytest.mark.parametrize("launch", [1, 2])
 @pytest.mark.parametrize("B,Tn,V", [(1100, 3, 4099), (2100, 2, 32128), (1500, 1, 32128), (3, 700, 32128),
                                     (37, 61, 32128)])
-def test_ragged_order_many_rollouts(B, Tn, V):
-    """k_ragged_order over several workgroups of rows (rollouts straddling them, one row per
-    rollout, rollouts longer than a workgroup's rows): the list is valid-first in row order,
-    the count follows, and the ordered launch gives the natural-order launch's bits (lengths
-    include 0 and values beyond T)."""
+def test_ragged_order_many_rollouts(B, Tn, V, launch):
+    """The ragged order over several workgroups of rows (rollouts straddling them, one row per
+    rollout, rollouts longer than a workgroup's rows), in both forms — k_ragged_order's one
+    launch and row_order.h's two chunk-count launches (the default past 64 chunks; tuning
+    "order_launch"): the list is valid-first in row order, the count follows, and the ordered
+    launch gives the natural-order launch's bits (lengths include 0 and values beyond T)."""
+    _lib.set_tuning("order_launch", launch)
+    try:
+        _ragged_order_case(B, Tn, V)
+    finally:
+        _lib.set_tuning("order_launch", 0)
+
+
+def _ragged_order_case(B, Tn, V):
     g = torch.Generator().manual_seed(B)
     x = torch.randn(B, Tn, V, generator=g).to(torch.bfloat16).to(DEV)
     y = torch.randint(0, V, (B, Tn), generator=g).to(DEV)

@@ -347,7 +347,9 @@ int check_launch(const char* what);
 // A ragged batch's row order (vocab_rows.hip k_ragged_order): rows (b, t < lengths[b]) first in
 // row order, then ~row of the padding rows, then the number of valid rows.  `order` holds
 // ragged_order_bytes(B, T) bytes.
-inline int64_t ragged_order_bytes(int64_t B, int64_t T) { return 4 * (B * T + 4); }
+inline int64_t ragged_order_bytes(int64_t B, int64_t T) {  // list + count + the chunk counts of row_order.h
+    return 4 * (B * T + 4 + (B * T + 1023) / 1024 + 1);
+}
 int launch_ragged_order(const int64_t* lengths, int64_t B, int64_t T, int* order, hipStream_t stream);
 
 }  // namespace trlx

@@ -34,6 +34,7 @@
 // the second product from ONE swizzled LDS image.
 #define TRLX_ROW_TAILS_NO_KERNELS
 #include "ppo_token.h"
+#include "row_order.h"
 
 namespace trlx {
 
@@ -84,7 +85,7 @@ struct LmLossArgs {
     const int64_t* labels;  // [N] (token rows)
     int64_t lb;             // label stride
     // compaction: rows[m] = row of compact token m < *nrows (mask != 0), ~row of the masked
-    // ones after them (k_mask_order); NULL = every token, row m
+    // ones after them (row_order.h launch_order); NULL = every token, row m
     const int* rows;
     const int* nrows;
     int nsplit;       // vocab splits of the forward: the maximum (nsplit_fixed: exactly)
@@ -1024,63 +1025,6 @@ __global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int
     }
 }
 
-// ------------------------------------------------------------------ mask compaction
-// order[0, nv) = rows with mask != 0 in row order, order[nv, N) = ~row of the others, order[N] =
-// nv.  Two launches over 1024-row chunks: per-chunk counts, then every chunk sums the counts
-// before it (O(N/1024) loads per workgroup) and places its rows.
-constexpr int kMaskChunk = 1024;
-__global__ __launch_bounds__(256) void k_mask_count(const int64_t* mask, int64_t n, int* cnt) {
-    __shared__ int s_red[4];
-    const int64_t p0 = int64_t(blockIdx.x) * kMaskChunk;
-    int c = 0;
-    for (int64_t p = p0 + threadIdx.x; p < min(p0 + kMaskChunk, n); p += blockDim.x) c += mask[p] != 0;
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) cnt[blockIdx.x] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-}
-__global__ __launch_bounds__(256) void k_mask_place(const int64_t* mask, int64_t n, const int* cnt, int nchunk,
-                                                    int* order) {
-    __shared__ int s_red[2][4];
-    __shared__ int s_scan[256];
-    const int tid = threadIdx.x;
-    int pre = 0, tot = 0;
-    for (int c = tid; c < nchunk; c += blockDim.x) {
-        tot += cnt[c];
-        pre += c < int(blockIdx.x) ? cnt[c] : 0;
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        tot += __shfl_xor(tot, off);
-        pre += __shfl_xor(pre, off);
-    }
-    if ((tid & 63) == 0) {
-        s_red[0][tid >> 6] = tot;
-        s_red[1][tid >> 6] = pre;
-    }
-    const int64_t p0 = int64_t(blockIdx.x) * kMaskChunk + 4 * tid;  // 4 consecutive rows per thread
-    int f[4], loc = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        f[e] = p0 + e < n && mask[p0 + e] != 0;
-        loc += f[e];
-    }
-    s_scan[tid] = loc;
-    __syncthreads();
-    const int nvalid = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
-    int run = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
-    for (int k = 0; k < tid; ++k) run += s_scan[k];  // valid rows before p0
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const int64_t p = p0 + e;
-        if (p >= n) break;
-        if (f[e])
-            order[run++] = int(p);
-        else
-            order[nvalid + int(p - run)] = ~int(p);
-    }
-    if (blockIdx.x == 0 && tid == 0) order[n] = nvalid;
-}
-
 // ------------------------------------------------------------------ host side
 static thread_local int g_ll_splits = 0;  // tuning "lmloss_splits" (0 = auto)
 static thread_local int g_ll_tsplit = 0;  // tuning "lmloss_dw_tsplit" (0 = auto)
@@ -1162,7 +1106,7 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w) {
     t.gbuf = reinterpret_cast<float*>(take(size_t(N) * 4));
     t.ybuf = reinterpret_cast<int*>(take(size_t(N) * 4));
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
-    t.cnt = reinterpret_cast<int*>(take(size_t((N + kMaskChunk - 1) / kMaskChunk + 1) * 4));
+    t.cnt = reinterpret_cast<int*>(take(size_t(order_chunks(N) + 1) * 4));
     t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 4 * 4));  // <= 4 waves per workgroup
     const LlDwPlan dp = ll_dw_plan(V);
     t.dwpart = reinterpret_cast<float*>(take(size_t(dp.nblk) * dp.tsplit * kLLTokBlock * H * 4));
@@ -1246,12 +1190,7 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.lddw = lddw;
     a.dw_dtype = dw_dtype;
     if (compact_mask) {
-        const int nchunk = int((N + kMaskChunk - 1) / kMaskChunk);
-        hipLaunchKernelGGL(k_mask_count, dim3(nchunk), dim3(256), 0, s, compact_mask, N, w.cnt);
-        rc = check_launch("k_mask_count");
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_mask_place, dim3(nchunk), dim3(256), 0, s, compact_mask, N, w.cnt, nchunk, w.order);
-        rc = check_launch("k_mask_place");
+        rc = launch_order<false>(compact_mask, 1, N, w.cnt, w.order, s);  // mask != 0 rows first
         if (rc) return rc;
         a.rows = w.order;
         a.nrows = w.order + N;

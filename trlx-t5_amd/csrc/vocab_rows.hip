@@ -15,6 +15,7 @@
 #include <hip/hip_ext.h>
 
 #include "ppo_token.h"
+#include "row_order.h"
 
 namespace trlx {
 
@@ -748,6 +749,7 @@ static thread_local int g_stream_threads = 0;
 static thread_local int g_stream_unroll = 0;
 static thread_local int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
 static thread_local int g_ragged_order = 0;      // forward rows with lengths: 0 auto (valid rows first), 1 natural
+static thread_local int g_order_launch = 0;  // ragged order: 0 auto, 1 one launch (k_ragged_order), 2 two (row_order.h)
 static thread_local int g_store_pol = 0;         // gradient-row stores: 0 auto, 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
 constexpr double kSC1Bytes = 1.5e9;  // auto: sc1 above this many gradient bytes per launch, else nt
 
@@ -995,10 +997,17 @@ size_t carve_ppo_workspace(void* base, int64_t B, int64_t T, Workspace* w) { ret
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled);  // lmhead_loss.hip
 
+// One launch while its workgroups' passes over all B lengths stay small (each reads every
+// length: O(B²·T / 1024) loads in all — 12 x 256 at C3); past kOrderOneLaunchChunks the two
+// chunk-count launches of row_order.h (O(B·T / 1024) loads per workgroup).
+constexpr int64_t kOrderOneLaunchChunks = 64;
 int launch_ragged_order(const int64_t* lengths, int64_t B, int64_t T, int* order, hipStream_t stream) {
     if (B * T == 0) return TRLX_OK;
-    hipLaunchKernelGGL(k_ragged_order, dim3(unsigned((B * T + kOrderPos - 1) / kOrderPos)), dim3(kOrderThreads), 0,
-                       stream, lengths, int(B), int(T), order, order + B * T);
+    const int64_t nchunk = (B * T + kOrderPos - 1) / kOrderPos;
+    if (g_order_launch == 2 || (g_order_launch == 0 && nchunk > kOrderOneLaunchChunks))
+        return launch_order<true>(lengths, int(T), B * T, order + B * T + 4, order, stream);
+    hipLaunchKernelGGL(k_ragged_order, dim3(unsigned(nchunk)), dim3(kOrderThreads), 0, stream, lengths, int(B),
+                       int(T), order, order + B * T);
     return check_launch("k_ragged_order");
 }
 
@@ -1406,6 +1415,9 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
     } else if (k == "split_mid") {
         TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG, "split_mid: 0..3");
         g_split_mid = int(value);
+    } else if (k == "order_launch") {
+        TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "order_launch: 0 auto, 1 one launch, 2 two launches");
+        g_order_launch = int(value);
     } else if (k == "ragged_order") {
         TRLX_REQUIRE(value == 0 || value == 1, TRLX_ERR_ARG, "ragged_order: 0 (valid rows first) or 1 (natural)");
         g_ragged_order = int(value);
