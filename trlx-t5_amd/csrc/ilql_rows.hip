@@ -414,6 +414,7 @@ __global__ __launch_bounds__(kIlqlRedThreads) void k_ilql_finalize(trlx_ilql_arg
 
 // ------------------------------------------------------------------ host side
 int tuning_split_lds();  // vocab_rows.hip ("split_lds")
+int tuning_ilql_split();  // vocab_rows.hip ("ilql_split")
 
 static const int kIlqlNVs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 16};
 
@@ -472,8 +473,13 @@ static int ilql_launch_rows(const trlx_ilql_args& a, hipStream_t stream) {
     if (es == 4 && tuning_split_lds() != 1) {  // long fp32 rows: split VGPR + LDS residency
         const int64_t nvec = a.V / 4 + 1 + (kLineVecs - 1);
         if (nvec > 512 * 16 && nvec <= 512 * (20 + 5)) {
-            hipLaunchKernelGGL((k_ilql_rows<DT, 20, 5>), dim3(unsigned(ilql_num_rows(a.B, a.L, a.A, a.nq))), dim3(512), 0,
-                               stream, a);
+            const dim3 grid(unsigned(ilql_num_rows(a.B, a.L, a.A, a.nq)));
+            switch (tuning_ilql_split()) {
+                case 1: hipLaunchKernelGGL((k_ilql_rows<DT, 22, 3>), grid, dim3(512), 0, stream, a); break;
+                case 2: hipLaunchKernelGGL((k_ilql_rows<DT, 21, 4>), grid, dim3(512), 0, stream, a); break;
+                case 3: hipLaunchKernelGGL((k_ilql_rows<DT, 19, 6>), grid, dim3(512), 0, stream, a); break;
+                default: hipLaunchKernelGGL((k_ilql_rows<DT, 20, 5>), grid, dim3(512), 0, stream, a); break;
+            }
             return check_launch("k_ilql_rows (split LDS)");
         }
     }

@@ -765,6 +765,8 @@ static int store_policy_for(double grad_bytes, bool split) {
 static thread_local int g_split_lds = 0;         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
 static thread_local int g_split_mid = 0;         // mid bf16 rows (loss / backward): 0 auto (= 3), 1 off, 2 5+3, 3 6+2
 int tuning_split_lds() { return g_split_lds; }
+static thread_local int g_ilql_split = 0;  // ILQL fp32 split residency: 0 = 20 VGPR + 5 LDS steps, 1 = 22 + 3, 2 = 21 + 4, 3 = 19 + 6
+int tuning_ilql_split() { return g_ilql_split; }
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the
 // workgroup size.  Default: 512-thread workgroups (8 waves) -- measured on MI355X (C2,
@@ -1406,6 +1408,9 @@ extern "C" int trlx_set_tuning(const char* key, int64_t value) {
         TRLX_REQUIRE(value == 0 || (value % kWave == 0 && value <= kStreamMaxThreads), TRLX_ERR_ARG,
                      "stream_threads must be a multiple of 64 <= %d", kStreamMaxThreads);
         g_stream_threads = int(value);
+    } else if (k == "ilql_split") {
+        TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG, "ilql_split: 0 (20+5), 1 (22+3), 2 (21+4), 3 (19+6)");
+        g_ilql_split = int(value);
     } else if (k == "split_lds") {
         TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "split_lds: 0..2");
         g_split_lds = int(value);
