@@ -236,3 +236,73 @@ def test_lm_head_logprobs_split_plans(splits, tsplit):
     assert _rel(got[1], dh64) < 1e-2 and _rel(got[2], dw64) < 1e-2
     torch.testing.assert_close(got[0], base[0], rtol=1e-6, atol=1e-5)
     assert _rel(got[1], base[1]) < 2e-3 and _rel(got[2], base[2]) < 2e-3
+
+
+def test_loss_from_hidden_gemm_route_matches_fused():
+    """route='gemm' (hipBLASLt bf16 logits -> the loss rows -> dh / dW GEMMs, the reference's
+    structure on the hot path's kernels) against the fused route on the same step: the loss,
+    stats and dvalues to the bf16 rounding of the logits, dh / dW to bf16 GEMM tolerance."""
+    B, T, V, H = 8, 24, 3000, 768
+    x = _ppo_inputs(B, T, V, H, 91, True)
+    d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in x.items()}
+    outs = {}
+    for route in ("fused", "gemm"):
+        hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+        o = hp.step_from_hidden(d["h"], d["w"], d["ref_h"], d["w"], d["new_h"], d["labels"], d["old_values"],
+                                d["values"], d["scores"], lengths=d["lengths"], mask=d["mask"], route="fused",
+                                loss_route=route)
+        torch.cuda.synchronize()
+        outs[route] = [t.clone() for t in o]
+    f, g = outs["fused"], outs["gemm"]
+    torch.testing.assert_close(g[0].reshape(()), f[0].reshape(()), rtol=2e-3, atol=1e-4)
+    torch.testing.assert_close(g[4], f[4], rtol=1e-4, atol=1e-6)
+    m = d["mask"].bool()
+    assert _rel(g[2][m], f[2][m]) < 2e-2 and _rel(g[3], f[3]) < 2e-2
+    assert (g[2][~m] == 0).all()
+
+
+def test_loss_from_hidden_any_hidden_size():
+    """H = 1024 (no fused build): loss_route 'auto' takes the gemm route; checked against the
+    oracle's loss side on bf16-rounded logits (the reference's own lm_head output dtype on the
+    T5 path; straight-through rounding so the oracle's autograd is the reference's)."""
+    B, T, V, H = 4, 16, 2500, 1024
+    x = _ppo_inputs(B, T, V, H, 17, True)
+    d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in x.items()}
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+    loss, stats, dh, dw, dv = hp.step_from_hidden(d["h"], d["w"], d["ref_h"], d["w"], d["new_h"], d["labels"],
+                                                 d["old_values"], d["values"], d["scores"], lengths=d["lengths"],
+                                                 mask=d["mask"])
+    torch.cuda.synchronize()
+    st = hp.adv_stats.cpu()
+    mu, var = P.modeling.moments_to_mean_var(st, unbiased=True)
+    adv_w = ((hp.adv_raw.cpu().double() - mu) * torch.rsqrt(var + 1e-8)).float()
+    hd = x["new_h"].float().to(DEV).requires_grad_(True)
+    wd = x["w"].float().to(DEV).requires_grad_(True)
+    vd = x["values"].to(DEV).requires_grad_(True)
+    lg = hd @ wd.t()
+    lg = lg + (lg.bfloat16().float() - lg).detach()
+    lp = orc.logprobs_from_logits(lg, x["labels"].to(DEV))
+    want, _ = orc.ppo_loss(lp, vd, hp.lp_old, x["old_values"].to(DEV), adv_w.to(DEV), hp.returns,
+                           x["mask"].to(DEV))
+    want.backward()
+    torch.testing.assert_close(loss.reshape(()), want.detach(), rtol=2e-3, atol=1e-4)
+    torch.testing.assert_close(dv, vd.grad, rtol=1e-4, atol=1e-6)
+    m = x["mask"].bool().to(DEV)
+    assert _rel(dh[m], hd.grad[m]) < 2e-2 and _rel(dw, wd.grad) < 2e-2
+
+
+def test_lm_head_logprobs_autograd_any_hidden_size():
+    """lm_head_logprobs with gradients at an H the fused backward is not built for (1024):
+    hipBLASLt bf16 logits + logprobs_from_logits under autograd, against fp64 (bf16-logits
+    tolerance)."""
+    N, H, V = 96, 1024, 2000
+    h, w, y = _operands(N, H, V, 23)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(8))
+    hg = h.to(DEV).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32)
+    (lp * gout.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
+    torch.testing.assert_close(lp.detach().double(), lp64, rtol=0, atol=6e-2)
+    assert _rel(hg.grad, dh64) < 2e-2 and _rel(wg.grad, dw64) < 2e-2

@@ -78,8 +78,9 @@ def lm_head_logprobs(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.T
     logprobs [...] of out_dtype (default: hidden.dtype, the dtype the reference's logits —
     and so its logprobs — have).  Arithmetic: bf16 products, fp32 accumulation and
     softmax statistics; the logits are not rounded to bf16 (the reference rounds them).
-    Differentiable w.r.t. hidden and weight when either requires grad (H in
-    GRAD_HIDDEN_SIZES): the backward runs lmhead_loss.hip's dh / dW passes."""
+    Differentiable w.r.t. hidden and weight when either requires grad: for H in
+    GRAD_HIDDEN_SIZES the backward runs lmhead_loss.hip's dh / dW passes (no [.., V] tensor);
+    other H take hipBLASLt bf16 logits + logprobs_from_logits (the reference's structure)."""
     _lib.require_cuda(hidden, weight, labels)
     if hidden.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
         raise TypeError("lm_head_logprobs takes bf16 hidden states and weight")
@@ -92,10 +93,13 @@ def lm_head_logprobs(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.T
         raise ValueError("labels must have hidden.shape[:-1]")
     dt = hidden.dtype if out_dtype is None else out_dtype
     if torch.is_grad_enabled() and (hidden.requires_grad or weight.requires_grad):
-        if H not in GRAD_HIDDEN_SIZES:
-            raise ValueError(f"lm_head_logprobs with gradients: hidden size {H} not built {GRAD_HIDDEN_SIZES}")
         if return_lse:
             raise ValueError("return_lse is for the no-grad (experience) path")
+        if H not in GRAD_HIDDEN_SIZES:
+            # the reference's own structure for the hidden sizes the fused backward is not built
+            # for: bf16 logits by hipBLASLt (autograd), the row kernels' logprobs_from_logits
+            from .modeling import logprobs_from_logits
+            return logprobs_from_logits(torch.matmul(hidden, weight.t()), labels).to(dt)
         return _LmHeadLogprobs.apply(hidden, weight, labels, dt)
     h, w, y = _operands(hidden, weight, labels)
     N, V = h.shape[0], w.shape[0]

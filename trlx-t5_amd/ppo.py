@@ -331,7 +331,8 @@ class PPOConfig:
         (accelerate_ppo_model.py:96-118 with the lm_head of ppo_models.py:640 / :274), the
         [.., V] logits and dlogits never in HBM: lm_head_logprobs' differentiable MFMA block
         feeds the PPO loss kernels, and backward() delivers d hidden, d weight (lm_head) and
-        d values.  hidden [.., H] / weight [V, H] bf16, H in lm_head.GRAD_HIDDEN_SIZES.
+        d values.  hidden [.., H] / weight [V, H] bf16 (H in lm_head.GRAD_HIDDEN_SIZES: the fused
+        backward; other H: hipBLASLt bf16 logits + the row kernels, the reference's structure).
         Returns (loss, stats) like loss(); logprobs are kept in fp32 (the reference's bf16
         logits give bf16 logprobs)."""
         lp = lm_head_logprobs(hidden, weight, labels, out_dtype=torch.float32)

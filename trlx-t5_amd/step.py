@@ -669,7 +669,7 @@ class PPOHotPath:
     LOSS_FROM_HIDDEN_SIZES = (512, 768)
 
     def policy_loss_from_hidden(self, hidden, weight, labels, values, old_values, mask=None,
-                                grad_dtype=torch.bfloat16):
+                                grad_dtype=torch.bfloat16, route="auto"):
         """K2 with the lm_head folded in (loss side): the policy's last hidden
         states [B, T, H] and lm_head weight [V, H] (bf16, H in LOSS_FROM_HIDDEN_SIZES) replace
         the logits — the reference's policy forward + logprobs_from_logits + PPO loss +
@@ -678,20 +678,31 @@ class PPOHotPath:
         launches and a per-token combine; tokens with mask == 0 are compacted out).  Returns
         (loss, stats, dhidden [B, T, H], dweight [V, H], dvalues), gradients in grad_dtype;
         the same loss tail (deferred / side stream) as policy_loss.  Unsplit whitening only (the
-        serial step(): experience / experience_from_hidden, then this)."""
-        if self._split_mode:
-            raise RuntimeError("policy_loss_from_hidden runs after the unsplit GAE (step / experience); "
-                               "split-beta / pipelined batches use policy_loss")
+        serial step(): experience / experience_from_hidden, then this).
+        route: "fused" (the kernels above; H in LOSS_FROM_HIDDEN_SIZES), "gemm" (the
+        reference's own structure on the hot path's kernels: hipBLASLt bf16 logits -> the fused
+        loss rows (policy_loss) -> hipBLASLt dh = dlogits·W and dW = dlogitsᵀ·h; any H, the
+        [B, T, V] logits and dlogits in HBM), "auto" = fused where it is built, else gemm."""
         B, T, V = self.B, self.T, self.V
         if hidden.dim() != 3 or tuple(hidden.shape[:2]) != (B, T) or weight.dim() != 2 or weight.shape[0] != V or \
                 weight.shape[1] != hidden.shape[2] or hidden.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
             raise ValueError(f"hidden {tuple(hidden.shape)}/{hidden.dtype} and weight {tuple(weight.shape)}/"
                              f"{weight.dtype} do not match the hot path ({B},{T},H) x ({V},H) bf16")
         H = hidden.shape[2]
-        if H not in self.LOSS_FROM_HIDDEN_SIZES:
-            raise ValueError(f"policy_loss_from_hidden: hidden size {H} not built {self.LOSS_FROM_HIDDEN_SIZES}")
         if grad_dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("grad_dtype must be bf16 or fp32")
+        if route not in ("auto", "fused", "gemm"):
+            raise ValueError(f"route must be auto, fused or gemm, not {route!r}")
+        if route == "auto":
+            route = "fused" if H in self.LOSS_FROM_HIDDEN_SIZES else "gemm"
+        if route == "gemm":
+            return self._policy_loss_from_hidden_gemm(hidden, weight, labels, values, old_values, mask, grad_dtype)
+        if H not in self.LOSS_FROM_HIDDEN_SIZES:
+            raise ValueError(f"policy_loss_from_hidden: fused route not built for hidden size {H} "
+                             f"{self.LOSS_FROM_HIDDEN_SIZES} (route='gemm' takes any H)")
+        if self._split_mode:
+            raise RuntimeError("policy_loss_from_hidden runs after the unsplit GAE (step / experience); "
+                               "split-beta / pipelined batches use policy_loss")
         _lib.require_cuda(hidden, weight)
         labels = self._int64(labels, (B, T), "labels")
         mask = self._int64(mask, (B, T), "mask", required=False)
@@ -728,14 +739,42 @@ class PPOHotPath:
         return self.loss, self.stats, dh, dw, self.dvalues
 
     def step_from_hidden(self, hidden, weight, ref_hidden, ref_weight, new_hidden, labels, old_values, values,
-                         scores, lengths=None, mask=None, group=None, route="auto", new_weight=None):
+                         scores, lengths=None, mask=None, group=None, route="auto", new_weight=None,
+                         loss_route="auto"):
         """step() from hidden states on both sides: experience_from_hidden
-        (policy + reference lm_head + logprobs, GAE) then policy_loss_from_hidden on the
-        updated policy's hidden states (new_weight: its lm_head, default `weight`)."""
+        (policy + reference lm_head + logprobs, GAE; `route`) then policy_loss_from_hidden on the
+        updated policy's hidden states (new_weight: its lm_head, default `weight`; `loss_route`)."""
         self.experience_from_hidden(hidden, weight, ref_hidden, ref_weight, labels, old_values, scores,
                                     lengths=lengths, mask=mask, group=group, route=route)
         return self.policy_loss_from_hidden(new_hidden, weight if new_weight is None else new_weight, labels, values,
-                                            old_values, mask=mask)
+                                            old_values, mask=mask, route=loss_route)
+
+    def _policy_loss_from_hidden_gemm(self, hidden, weight, labels, values, old_values, mask, grad_dtype):
+        """policy_loss_from_hidden's gemm route: hipBLASLt bf16 logits (the reference's lm_head
+        output dtype on the T5 path), the fused loss rows, hipBLASLt dh / dW GEMMs."""
+        B, T, V = self.B, self.T, self.V
+        H = hidden.shape[2]
+        N = B * T
+        if getattr(self, "loss_logits", None) is None or self.loss_logits.shape != (B, T, V):
+            self.loss_logits = torch.empty((B, T, V), dtype=torch.bfloat16, device=self.device)
+        torch.matmul(hidden, weight.t(), out=self.loss_logits)
+        loss, stats, dl, dv = self.policy_loss(self.loss_logits, labels, values, old_values, mask=mask)
+        d2 = dl.reshape(N, V)
+        h2 = hidden.reshape(N, H)
+        if getattr(self, "dhidden", None) is None or self.dhidden.shape != (B, T, H) or self.dhidden.dtype != grad_dtype:
+            self.dhidden = torch.empty((B, T, H), dtype=grad_dtype, device=self.device)
+            self.dweight = torch.empty((V, H), dtype=grad_dtype, device=self.device)
+        if grad_dtype == torch.bfloat16:
+            torch.matmul(d2, weight, out=self.dhidden.view(N, H))
+            torch.matmul(d2.t(), h2, out=self.dweight)
+        else:
+            self.dhidden.view(N, H).copy_(torch.matmul(d2, weight))
+            self.dweight.copy_(torch.matmul(d2.t(), h2))
+        return loss, stats, self.dhidden, self.dweight, dv
+
+    def release_loss_logits(self):
+        """Free the policy_loss_from_hidden gemm route's [B, T, V] logits (re-allocated on next use)."""
+        self.loss_logits = None
 
     def release_lm_logits(self):
         """Free the gemm route's [2, chunk, T, V] logits ring (re-allocated on next use)."""
