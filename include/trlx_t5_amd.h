@@ -80,6 +80,7 @@ const char* trlx_last_error(void);
  *   "lmloss_splits"     fused loss forward vocab splits: 0 auto (the fullest last round), 1..8 fixed
  *   "lmloss_dw_tsplit"  fused loss dW: 0 auto (the last round's vocab blocks split over the tokens),
  *                       1 = no split, 2..16 = that many token splits
+ *   "lmloss_fwd"        fused loss forward form: 0 auto (= 1), 1 = 32x32x16 wave pairs, 2 = 16x16x32 waves
  *   "store_policy"      gradient-row store cache policy: 0 auto (default: nt; sc1 for all-VGPR rows
  *                       launches writing > 1.5 GB), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
  * Results are identical up to fp32 summation order; only speed changes. */

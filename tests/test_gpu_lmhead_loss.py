@@ -306,3 +306,31 @@ def test_lm_head_logprobs_autograd_any_hidden_size():
     lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
     torch.testing.assert_close(lp.detach().double(), lp64, rtol=0, atol=6e-2)
     assert _rel(hg.grad, dh64) < 2e-2 and _rel(wg.grad, dw64) < 2e-2
+
+
+@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("N,H,V", [(200, 768, 7000), (70, 512, 33), (300, 768, 50257)])
+def test_lm_head_logprobs_forward_forms(form, N, H, V):
+    """Both forward forms (tuning lmloss_fwd: 1 = the 32x32x16 pair form with the group-sum
+    exchange, the default, 2 = the 16x16x32 one-wave-per-16-tokens form) against fp64, and
+    the restart path of each (a logit jump of ~80 from the 3rd tile on)."""
+    P._lib.set_tuning("lmloss_fwd", form)
+    try:
+        for jump in (False, True):
+            h, w, y = _operands(N, H, V, N + form)
+            if jump and V > 96:
+                wf = w.float()
+                dvec = h.float().mean(0)
+                wf[2 * 32:] += 80.0 * dvec / (dvec @ dvec)
+                w = wf.to(torch.bfloat16)
+            gout = torch.randn(N, generator=torch.Generator().manual_seed(form))
+            hg = h.to(DEV).requires_grad_(True)
+            wg = w.to(DEV).requires_grad_(True)
+            lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32)
+            (lp * gout.to(DEV)).sum().backward()
+            torch.cuda.synchronize()
+            lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
+            torch.testing.assert_close(lp.detach().double(), lp64, rtol=1e-5, atol=1e-4)
+            assert _rel(hg.grad, dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
+    finally:
+        P._lib.set_tuning("lmloss_fwd", 0)

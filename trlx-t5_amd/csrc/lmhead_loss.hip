@@ -353,6 +353,35 @@ struct LlGeom {
 typedef LlGeom<768, 2, 2> LlG768;
 typedef LlGeom<512, 2, 2> LlG512;
 
+// ------------------------------------------------------------------ 16x16x32 operand reads
+// Per-lane byte offsets in a staged 32-row tile (subtile image, ll_off) for
+// v_mfma_f32_16x16x32_bf16, lane (g, c) = (lane >> 4, lane & 15), q = (lane >> 2) & 3, p = lane & 3:
+//   row read of tile row 16mb + c, columns 32ks + 8g (the A operand of an M = rows product):
+//     ll16_rb + 4096mb + (ks>>2)·8192 + (ks&3)·512
+//   transposed read of rows 4g + q and 16 + 4g + q, columns 16nb + 4p (a K = 32-row operand
+//   whose k slots are permuted: slot 8g + j = row 4g + j (j < 4) / 16 + 4g + j − 4 — the
+//   rows a lane holds of a 16x16 accumulator pair, see k_lmloss_dw):
+//     ll16_trb[nb&1] + (nb>>3)·8192 + ((nb&7)>>1)·512 (+4096)
+__device__ __forceinline__ int ll16_rb(int lane) {
+    const int g = lane >> 4, c = lane & 15;
+    return 2048 * (c >> 3) + 64 * (c & 7) + 16 * (g ^ ((c >> 2) & 3));
+}
+__device__ __forceinline__ int ll16_trb(int lane, int par) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    return 2048 * (g >> 1) + 64 * (4 * (g & 1) + q) + 16 * ((2 * par + (p >> 1)) ^ g) + 8 * (p & 1);
+}
+__device__ __forceinline__ bf16x8_t ll16_row_frag(const char* tile, int rb, int mb, int ks) {
+    return *reinterpret_cast<const bf16x8_t*>(tile + rb + 4096 * mb + (ks >> 2) * 8192 + (ks & 3) * 512);
+}
+__device__ __forceinline__ bf16x8_t ll16_tr_frag(const char* tile, const int* trb, int nb) {
+    typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+    const char* base = tile + trb[nb & 1] + (nb >> 3) * 8192 + ((nb & 7) >> 1) * 512;
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base);
+    const s16x4_t hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + 4096));
+    const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi4.x, hi4.y, hi4.z, hi4.w};
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+
 // Vocab splits of the forward for ntb live token blocks: the count (<= a.nsplit) whose last
 // round of workgroups is fullest — cost = ceil(ntb·ns / ncu) / ns rounds of one whole-vocab
 // block; ties go to more splits.  A pure function of the device-side token count, so the
@@ -641,11 +670,195 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
     }
 }
 
+// ------------------------------------------------------------------ forward, 16x16x32 form
+// One wave per 16 tokens over the WHOLE hidden dimension (h fragments 96 registers, O 192 at
+// H = 768), the k_lmloss_dw layout with the roles swapped, so no partial S crosses waves and a
+// step has one barrier.  Per 32-row W tile, on v_mfma_f32_16x16x32_bf16:
+//   S[v][t] = Σ_d W[v][d]·h[t][d]     2 vocab blocks x H/32 k-steps (W rows the A operand, the
+//                                     h fragments the B operand): lane (g, c) ends with vocab
+//                                     rows 16mb + 4g + r of token c
+//   P = 2^(S·log2e − offset·log2e)    8 values a lane; the token's offset is the first tile's
+//                                     max over its 4 lanes (g), fixed for the split, as ll_fwd_block
+//   Oᵀ[d][t] += Σ_v W[v][d]·P[v][t]   H/16 column blocks x one permuted k-step (W read
+//                                     transposed: the A operand; the lane's own 8 P values: B)
+// Software-pipelined one tile deep over a 3-stage ring (S(t+1) beside softmax(t), O(t) beside
+// nothing but tile t+2's DMA).
+template <class G, bool RESTART>
+__device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit,
+                                               int nv) {
+    constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI, kStage = G::kStage;
+    constexpr int NG = 2 * KS;  // S-phase gaps
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, c = lane & 15;
+    const int split = lin / ntb, mt = lin - split * ntb;
+    const int tm = mt * kLLTokBlock + wave * 16 + c;  // this lane's token (compact index)
+    const bool valid = tm < nv;
+    const int tc = valid ? tm : nv - 1;
+    const int row = a.rows ? a.rows[tc] : tc;
+    bf16x8_t hf[KS];  // B operand of S: lane (g, c) -> h[token c][32ks + 8g .. +7]
+    {
+        const uint16_t* hp = a.h + int64_t(row) * a.ldh + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) hf[ks] = *reinterpret_cast<const bf16x8_t*>(hp + 32 * ks);
+    }
+    const int nvt = (a.V + kLLRows - 1) / kLLRows;
+    const int t0 = int(int64_t(split) * nvt / nsplit), t1 = int(int64_t(split + 1) * nvt / nsplit);
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
+    auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
+        const int i = wave + G::kWaves * k;
+        const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
+        ll_piece(slot, i, rw, t < t1 ? off : int(0x7ffff000), lane);
+    };
+    const int rb = ll16_rb(lane);
+    const int trb[2] = {ll16_trb(lane, 0), ll16_trb(lane, 1)};
+    float mfix = -INFINITY, mtrue = -INFINITY, lrun = 0.0f;
+    if (RESTART) mfix = a.mlpart[int64_t(split) * a.N + tc].x;  // the true max pass 0 found
+    bool bad = false;
+    f32x4_t O[DB];  // Oᵀ[16nb + 4g + r][token c]
+#pragma unroll
+    for (int nb = 0; nb < DB; ++nb) O[nb] = f32x4_t{};
+    f32x4_t s[2];  // S of the tile whose softmax comes next
+    float x[8], pr[8], m4 = 0.0f, nm = 0.0f, ls = 0.0f;
+    // softmax of tile t in chunks (chunk k of 12): 0 = the lane's max + the token max over its
+    // four lanes, 1 = offset / overflow flag, 2..9 = one exp each, 10 = the row sum
+    auto sm_chunk = [&](int k, int t, auto mask_tag) __attribute__((always_inline)) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        if (k == 0) {
+            const int lim = a.V - t * kLLRows - 4 * g;  // vocab row 16mb + 4g + r exists iff 16mb + r < lim
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float v = s[e >> 2][e & 3];
+                x[e] = (!MASK || 16 * (e >> 2) + (e & 3) < lim) ? v : -INFINITY;
+            }
+            const float lm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])),
+                                   fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
+            m4 = fmaxf(lm, __shfl_xor(lm, 16));
+            m4 = fmaxf(m4, __shfl_xor(m4, 32));
+        } else if (k == 1) {
+            if (!RESTART) {
+                mtrue = fmaxf(mtrue, m4);
+                mfix = t == t0 ? m4 : mfix;
+                bad = bad || m4 > mfix + kLLOverflow;
+            }
+            nm = -mfix * kLog2e;
+            ls = 0.0f;
+        } else if (k < 10) {
+            const int e = k - 2;
+            pr[e] = exp2_fast(fmaf(x[e], kLog2e, nm));
+            ls += pr[e];
+        } else if (k == 10) {
+            lrun += ls;
+        }
+    };
+    auto s_mfma = [&](const char* tile, bf16x8_t* af, int k) __attribute__((always_inline)) {
+        const int mb = k / KS, ks = k % KS;
+        s[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], hf[ks], s[mb], 0, 0, 0);
+    };
+    // step t (t + 1 < t1): restrict LDS regions (alias scopes, as ll_fwd_block)
+    auto step = [&](const char* __restrict__ cur, const char* __restrict__ nx, char* __restrict__ fut, int t)
+                    __attribute__((always_inline)) {
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t+1
+        ll_lds_barrier();  // every wave's; every wave is done with tile t-1
+        constexpr int PF = 4;
+        bf16x8_t af[NG];
+#pragma unroll
+        for (int k = 0; k < PF; ++k) af[k] = ll16_row_frag(nx, rb, k / KS, k % KS);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = s[e >> 2][e & 3];  // S(t) for the softmax; S(t+1) accumulates anew
+        s[0] = f32x4_t{};
+        s[1] = f32x4_t{};
+        bf16x8_t pb;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            if (k + PF < NG) af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
+            s_mfma(nx, af, k);
+            if (k == 0) {  // the lane's max + token max (no mask inside the loop: see ll_fwd_block)
+                const float lm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])),
+                                       fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
+                m4 = fmaxf(lm, __shfl_xor(lm, 16));
+                m4 = fmaxf(m4, __shfl_xor(m4, 32));
+            } else if (k == 2) {
+                sm_chunk(1, t, std::false_type{});
+            } else if (k >= 3 && k < 11) {
+                sm_chunk(k - 1, t, std::false_type{});
+            } else if (k == 11) {
+                sm_chunk(10, t, std::false_type{});
+                pb = pack8(pr);
+            }
+            if ((k & 3) == 1 && (k >> 2) < NI) issue_piece(t + 2, fut, k >> 2);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- O(t): tr reads of tile t's W (cur) | MFMA
+        constexpr int PFO = 4;
+        bf16x8_t tf[DB];
+#pragma unroll
+        for (int nb = 0; nb < PFO; ++nb) tf[nb] = ll16_tr_frag(cur, trb, nb);
+#pragma unroll
+        for (int nb = 0; nb < DB; ++nb) {
+            if (nb + PFO < DB) tf[nb + PFO] = ll16_tr_frag(cur, trb, nb + PFO);
+            O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[nb], pb, O[nb], 0, 0, 0);
+            const int gk = NG + nb;
+            if ((gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 2, fut, gk >> 2);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    if (t0 < t1) {
+        char* c0 = smem;
+        char* c1 = smem + kStage;
+        char* c2 = smem + 2 * kStage;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) issue_piece(t0, c0, k);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) issue_piece(t0 + 1, c1, k);
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI));  // tile t0 (t0+1 may fly)
+        ll_lds_barrier();
+        s[0] = f32x4_t{};
+        s[1] = f32x4_t{};
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const bf16x8_t af = ll16_row_frag(c0, rb, k / KS, k % KS);
+            s[k / KS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, hf[k % KS], s[k / KS], 0, 0, 0);
+        }
+        for (int t = t0; t + 1 < t1; ++t) {
+            step(c0, c1, c2, t);
+            char* cc = c0;
+            c0 = c1;
+            c1 = c2;
+            c2 = cc;
+        }
+        // the last tile: its (masked) softmax and O product
+#pragma unroll
+        for (int k = 0; k < 11; ++k) sm_chunk(k, t1 - 1, std::true_type{});
+        const bf16x8_t pb = pack8(pr);
+#pragma unroll
+        for (int nb = 0; nb < DB; ++nb)
+            O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ll16_tr_frag(c0, trb, nb), pb, O[nb], 0, 0, 0);
+    }
+    // per-wave overflow flag (ll_fwd_block); the token's true max and Σ over its four lanes
+    bool any = false;
+    if (!RESTART) {
+        any = __any(bad);
+        if (lane == 0) a.flags[lin * G::kWaves + wave] = any;
+    }
+    float mt4 = fmaxf(mtrue, __shfl_xor(mtrue, 16));
+    mt4 = fmaxf(mt4, __shfl_xor(mt4, 32));
+    const float mrun = any ? mt4 : mfix;
+    float lt = lrun + __shfl_xor(lrun, 16);
+    lt = lt + __shfl_xor(lt, 32);
+    if (valid) {
+        float* op = a.opart + (int64_t(split) * a.N + tm) * a.H + 4 * g;
+#pragma unroll
+        for (int nb = 0; nb < DB; ++nb) *reinterpret_cast<f32x4_t*>(op + 16 * nb) = O[nb];
+        if (g == 0) a.mlpart[int64_t(split) * a.N + tm] = make_float2(mrun, lt);
+    }
+}
+
 // The first launch: one (token block, split) per workgroup; the split count follows the live
 // token count (ll_fwd_splits), and each XCD (blockIdx % 8) takes a contiguous run of the
 // split-major order, so the workgroups sharing an L2 stream the same W rows.  The RESTART
 // launch (one workgroup per CU) walks the blocks and reruns the flagged ones.
-template <class G, bool RESTART>
+template <class G, bool RESTART, bool F16>
 __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[3 * G::kStage + G::kWaves * 4096];
     static_assert(3 * G::kStage + G::kWaves * 4096 <= 163840, "forward LDS: 3 stages + exchange");
@@ -657,7 +870,10 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
         const int per_xcd = (total + 7) / 8;
         const int kx = int(blockIdx.x) >> 3, lin = (int(blockIdx.x) & 7) * per_xcd + kx;
         if (kx >= per_xcd || lin >= total) return;  // past an XCD's share / the live tokens
-        ll_fwd_block<G, false>(a, smem, lin, ntb, nsplit, nv);
+        if (F16)
+            ll_fwd16_block<G, false>(a, smem, lin, ntb, nsplit, nv);
+        else
+            ll_fwd_block<G, false>(a, smem, lin, ntb, nsplit, nv);
         return;
     }
     for (int lin = int(blockIdx.x); lin < total; lin += int(gridDim.x)) {
@@ -665,7 +881,10 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
 #pragma unroll
         for (int w = 0; w < G::kWaves; ++w) f |= a.flags[lin * G::kWaves + w];
         if (!f) continue;
-        ll_fwd_block<G, true>(a, smem, lin, ntb, nsplit, nv);
+        if (F16)
+            ll_fwd16_block<G, true>(a, smem, lin, ntb, nsplit, nv);
+        else
+            ll_fwd_block<G, true>(a, smem, lin, ntb, nsplit, nv);
         ll_lds_barrier();  // every wave is done with the LDS before the next block reuses it
     }
 }
@@ -806,48 +1025,65 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
 }
 
 // ------------------------------------------------------------------ dW
-// Workgroup = NG·32 vocab rows x one token split; the W fragments of its rows stay in
-// registers, 32-token tiles of h (+ their lse / g / label) stream through LDS:
-//   S[t][v] = Σ_d h[t][d]·W[v][d]        (group-summed over hidden slices, as in the forward)
-//   dS = g_t·(1[y_t = v] − 2^(S·log2e − lse_t·log2e))  -> bf16, the A operand of
-//   dW[v][d] += Σ_t dS[t][v]·h[t][d]     (OB d-blocks x 2 k-steps, h read transposed)
+// Workgroup = 64 vocab rows x one token split, one wave per 16 rows holding them over the
+// WHOLE hidden dimension (W fragments 96 registers, dW accumulators 192 at H = 768), so no
+// partial S is ever exchanged between waves.  32-token tiles of h (+ their −lse·log2e, g, y)
+// stream through LDS; per tile, on v_mfma_f32_16x16x32_bf16:
+//   Sᵀ[t][v] = Σ_d h[t][d]·W[v][d]       2 token blocks x H/32 k-steps; h read by rows (A), the
+//                                         W fragments the B operand: lane (g, c) ends with
+//                                         tokens 16·mb + 4g + r of vocab row c
+//   dS = g_t·(1[y_t = v] − 2^(S·log2e − lse_t·log2e))  — 8 tokens a lane, the scalars of 8 tokens
+//   dW[v][d] += Σ_t dS[v][t]·h[t][d]     H/16 column blocks x ONE k-step of 32 tokens whose k
+//                                         slots are permuted to what the lane holds: slot 8g + j
+//                                         = token 4g + j (j < 4) / 16 + 4g + j − 4 — the A
+//                                         operand is the lane's own 8 dS values, the B operand two
+//                                         transposed reads (rows 4g.., 16 + 4g..) of the tile
+// Twice the h bytes read from LDS per MFMA of the 32x32 pair form (each wave reads the whole
+// tile, for S and for dW), in exchange for no group sum, no barrier inside the tile and the
+// dS of one block computed beside the other block's MFMAs.
 template <class G>
-__global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
-    constexpr int HS = G::HS, KS = G::KS, OB = G::OB, NI = G::NI, H = G::H;
+__global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
+    constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI;
     constexpr int kStage = G::kStage + 768;  // h tile + {-lse·log2e, g, y} x 64 lanes
-    __shared__ __attribute__((aligned(16))) char smem[2 * kStage + G::kWaves * 4096];
-    char* xbuf = smem + 2 * kStage;
+    static_assert(G::kWaves == 4, "dW: four 16-row waves per 64-row workgroup");
+    __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), grp = wave / G::NW, sq = wave % G::NW;
-    const int hi = lane >> 5, c32 = lane & 31;
-    const LlLane LL = ll_lane(lane);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, c = lane & 15;
     const int nv = a.rows ? *a.nrows : a.N;
-    const int vpw = 32 * G::NG;
+    const int vpw = 64;
     // a whole vocab block over every token, or (the last round) a token split of one
     const bool part = int(blockIdx.x) >= a.dw_full;
     const int j = int(blockIdx.x) - a.dw_full;
     const int vb = part ? a.dw_full + j / a.tsplit : int(blockIdx.x);
     const int ts = part ? j % a.tsplit : 0, nts = part ? a.tsplit : 1;
-    const int v0 = vb * vpw + grp * 32;
+    const int v0 = vb * vpw + wave * 16;  // this wave's 16 vocab rows
+    const int vcol = v0 + c;
     const int ntt = (nv + kLLRows - 1) / kLLRows;
     const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
-    bf16x8_t wf[KS];  // B operand of S: lane -> vocab row v0 + c32, hidden sq·HS + 16ks + 8hi + j
-    {
-        const int vr = v0 + c32;
-        if (vr < a.V) {
-            const uint16_t* wp = a.w + int64_t(vr) * a.ldw + sq * HS + 8 * hi;
+    bf16x8_t wf[KS];  // B operand of Sᵀ: lane (g, c) -> W[v0 + c][32ks + 8g .. +7]
+    if (vcol < a.V) {
+        const uint16_t* wp = a.w + int64_t(vcol) * a.ldw + 8 * g;
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) wf[ks] = *reinterpret_cast<const bf16x8_t*>(wp + 16 * ks);
-        } else {
+        for (int ks = 0; ks < KS; ++ks) wf[ks] = *reinterpret_cast<const bf16x8_t*>(wp + 32 * ks);
+    } else {
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) wf[ks] = bf16x8_t{};
-        }
+        for (int ks = 0; ks < KS; ++ks) wf[ks] = bf16x8_t{};
     }
-    // the tile rows this lane's DMA pieces fetch (pieces i = wave + kWaves·k: two distinct rows),
-    // as byte offsets into h; with compaction the row indices are loaded a tile ahead
+    // per-lane byte offsets in a staged tile (subtile image, ll_off):
+    //   row read of token 16mb + c, columns 32ks + 8g: rb + 4096mb + (ks>>2)·8192 + (ks&3)·512
+    //   transposed read of rows 4g + q (+16), columns 16nb + 4p: trb[nb&1] + (nb>>3)·8192 +
+    //   ((nb&7)>>1)·512 (+4096)
+    const int rb = ll16_rb(lane);
+    const int trb[2] = {ll16_trb(lane, 0), ll16_trb(lane, 1)};
+    auto row_frag = [&](const char* tile, int mb, int ks) __attribute__((always_inline)) {
+        return ll16_row_frag(tile, rb, mb, ks);
+    };
+    auto tr_frag = [&](const char* tile, int nb) __attribute__((always_inline)) { return ll16_tr_frag(tile, trb, nb); };
+    // the tile rows this lane's DMA pieces fetch (pieces i = wave + 4k: two distinct rows)
     auto tok_row = [&](int m) { const int mc = min(m, nv - 1); return a.rows ? a.rows[mc] : mc; };
-    const int rA = ll_piece_row(wave, lane), rB = ll_piece_row(wave + G::kWaves, lane);
     int rowA = 0, rowB = 0, nrowA = 0, nrowB = 0;
+    const int rA = ll_piece_row(wave, lane), rB = ll_piece_row(wave + G::kWaves, lane);
     if (t0 < t1) {
         rowA = tok_row(t0 * kLLRows + rA);
         rowB = tok_row(t0 * kLLRows + rB);
@@ -858,17 +1094,16 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
     const __amdgpu_buffer_rsrc_t rnl = make_rsrc(a.nlse, uint32_t(a.N) * 4u);
     const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gbuf, uint32_t(a.N) * 4u);
     const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.ybuf, uint32_t(a.N) * 4u);
-    // DMA piece k of tile t (rows ra / rb) into slot; a tile past the split fetches nothing
-    auto issue_piece = [&](int t, char* slot, int k, int ra, int rb) __attribute__((always_inline)) {
+    auto issue_piece = [&](int t, char* slot, int k, int ra, int rbw) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
-        const int off = ll_piece_src(i, (((i & 7) == (wave & 7)) ? ra : rb) * int(a.ldh) * 2, lane);
+        const int off = ll_piece_src(i, (((i & 7) == (wave & 7)) ? ra : rbw) * int(a.ldh) * 2, lane);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
                                                  t < t1 ? off : int(0x7ffff000), 0, 0, 0);
     };
-    // token scalars of tile t (wave 0): {-lse·log2e, g, y} of token min(t·32 + c32, nv-1) in
-    // lanes c32 and c32+32 alike
+    // token scalars of tile t (wave 0): {-lse·log2e, g, y} of token min(t·32 + l&31, nv-1) in
+    // lanes l and l+32 alike
     auto issue_scalars = [&](int t, char* slot) __attribute__((always_inline)) {
-        const int mi = (t < t1 ? min(t * kLLRows + c32, nv - 1) : 0x1fffffff) * 4;
+        const int mi = (t < t1 ? min(t * kLLRows + (lane & 31), nv - 1) : 0x1fffffff) * 4;
         char* sc = slot + G::kStage;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rnl, (__attribute__((address_space(3))) void*)sc, 4, mi, 0, 0, 0);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (__attribute__((address_space(3))) void*)(sc + 256), 4, mi, 0, 0,
@@ -876,132 +1111,98 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_dw(LmLossArgs a) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (__attribute__((address_space(3))) void*)(sc + 512), 4, mi, 0, 0,
                                                  0);
     };
-    f32x16_t D[OB];
+    f32x4_t D[DB];  // dW[v0 + 4g + r][16nb + c]
 #pragma unroll
-    for (int b = 0; b < OB; ++b) D[b] = f32x16_t{};
+    for (int nb = 0; nb < DB; ++nb) D[nb] = f32x4_t{};
     if (t0 < t1) {
 #pragma unroll
         for (int k = 0; k < NI; ++k) issue_piece(t0, smem, k, rowA, rowB);
         if (wave == 0) issue_scalars(t0, smem);
     }
-    const int vcol = v0 + c32;
-    // One tile, its schedule written out gap by gap (sched_barrier fences, as the forward's step):
-    //   S phase, gap k: row read k+4 | MFMA k of S(t) | every 3rd gap one DMA piece of tile t+1
-    //   exchange: the partial S written, barrier, the group's partials read and summed
-    //   dS of the tile's first 16 tokens (k-step 0) from S and the staged scalars
-    //   dW phase, gap i (k-step-major): tr read i+4 | dS of token half 2 (gaps 0-7, one value a
-    //     gap, packed at gap 7 for the k-step-1 MFMAs from gap OB) | MFMA i | DMA pieces left
-    auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, char* __restrict__ xb, int t) __attribute__((always_inline)) {
-        const int pa = nrowA, pb = nrowB;  // tile t+1's rows (loaded a tile ago)
-        if (a.rows) {  // tile t+2's rows for the next call: their loads retire during this tile
-            nrowA = tok_row((t + 2) * kLLRows + rA);
-            nrowB = tok_row((t + 2) * kLLRows + rB);
-        } else {
-            nrowA = min((t + 2) * kLLRows + rA, nv - 1);
-            nrowB = min((t + 2) * kLLRows + rB, nv - 1);
-        }
-        const char* hs = cur + sq * HS * 64;
-        constexpr int PF = 4;
-        bf16x8_t af[KS];
-#pragma unroll
-        for (int k = 0; k < PF; ++k) af[k] = ll_row_frag(hs, LL, k);
-        f32x16_t s = f32x16_t{};
-        // this tile's token scalars into registers during the S phase (12 b128 reads of the
-        // staged {-lse·log2e, g, y}: tokens 8q + 4hi .. +3 for q = 0..3)
+    constexpr int NG = 2 * KS;  // S-phase gaps
+    // one tile; the LDS regions as __restrict__ parameters (alias scopes, as the forward)
+    // tile t+2's rows: loaded unconditionally (a zero-size resource without compaction), picked
+    // at the next tile — a load under a branch made hipcc wait for it at the branch's join
+    const __amdgpu_buffer_rsrc_t rrows = make_rsrc(a.rows, a.rows ? uint32_t(a.N) * 4u : 0u);
+    auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, int t) __attribute__((always_inline)) {
+        const int pa = a.rows ? nrowA : min((t + 1) * kLLRows + rA, nv - 1);  // tile t+1's rows
+        const int pb = a.rows ? nrowB : min((t + 1) * kLLRows + rB, nv - 1);
+        nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 2) * kLLRows + rA, nv - 1) * 4, 0, 0);
+        nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 2) * kLLRows + rB, nv - 1) * 4, 0, 0);
         const char* scb = cur + G::kStage;
-        f32x4_t snl[4], sgg[4];
-        int4 syy[4];
+        f32x4_t snl[2], sgg[2];
+        int4 syy[2];
+        f32x4_t sacc[2] = {f32x4_t{}, f32x4_t{}};
+        float ds[8];
+        auto dsv = [&](int mb, int r) __attribute__((always_inline)) {
+            const int tb = 16 * mb + 4 * g + r;  // token of the tile
+            const float gv = t * kLLRows + tb < nv ? sgg[mb][r] : 0.0f;
+            const float pv = exp2_fast(fmaf(sacc[mb][r], kLog2e, snl[mb][r]));
+            ds[4 * mb + r] = gv * ((syy[mb][r] == vcol ? 1.0f : 0.0f) - pv);
+        };
+        // ---- S phase: gap k = 24mb + ks (mb-major): row read k+PF | MFMA | DMA piece every
+        // 4th gap | the tile's scalars read in gaps 2..7 | dS of block 0 in the gaps of block 1
+        constexpr int PF = 4;
+        bf16x8_t af[NG];
 #pragma unroll
-        for (int k = 0; k < KS; ++k) {
-            if (k + PF < KS) af[k + PF] = ll_row_frag(hs, LL, k + PF);
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[k], wf[k], s, 0, 0, 0);
-            if (k % 3 == 1 && k / 3 < NI) issue_piece(t + 1, nxt, k / 3, pa, pb);
-            if (k >= KS - 12) {
-                const int q = (k - (KS - 12)) & 3, tb = 8 * q + 4 * hi;
-                const int which = (k - (KS - 12)) >> 2;
-                if (which == 0) snl[q] = *reinterpret_cast<const f32x4_t*>(scb + 4 * tb);
-                else if (which == 1) sgg[q] = *reinterpret_cast<const f32x4_t*>(scb + 256 + 4 * tb);
-                else syy[q] = *reinterpret_cast<const int4*>(scb + 512 + 4 * tb);
+        for (int k = 0; k < PF; ++k) af[k] = row_frag(cur, k / KS, k % KS);
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            if (k + PF < NG) af[k + PF] = row_frag(cur, (k + PF) / KS, (k + PF) % KS);
+            const int mb = k / KS, ks = k % KS;
+            sacc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], wf[ks], sacc[mb], 0, 0, 0);
+            if ((k & 3) == 1 && (k >> 2) < NI) issue_piece(t + 1, nxt, k >> 2, pa, pb);
+            if (k >= 2 && k < 8) {
+                const int n = k - 2, b2 = n & 1;
+                if (n < 2) snl[b2] = *reinterpret_cast<const f32x4_t*>(scb + 4 * (16 * b2 + 4 * g));
+                else if (n < 4) sgg[b2] = *reinterpret_cast<const f32x4_t*>(scb + 256 + 4 * (16 * b2 + 4 * g));
+                else syy[b2] = *reinterpret_cast<const int4*>(scb + 512 + 4 * (16 * b2 + 4 * g));
             }
+            if (k >= KS + 4 && k < KS + 8) dsv(0, k - KS - 4);  // block 0's S is final (+latency)
             __builtin_amdgcn_sched_barrier(0);
         }
         if (wave == 0) issue_scalars(t + 1, nxt);
-        ll_group_write(s, xb, wave, lane);
-        ll_lds_barrier();
-        // the group's partials, all read now; the first half summed here, the second half in the
-        // first dW gap (its reads land behind the first half's dS)
-        f32x4_t xv[4][G::NW];
-        {
-            const f32x4_t* o = reinterpret_cast<const f32x4_t*>(xb + (wave - wave % G::NW) * 4096);
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int jj = 0; jj < G::NW; ++jj) xv[q][jj] = o[jj * 256 + q * 64 + lane];
-        }
-        auto xsum = [&](int q) __attribute__((always_inline)) {
-            f32x4_t v = xv[q][0];
-#pragma unroll
-            for (int jj = 1; jj < G::NW; ++jj) v += xv[q][jj];
-            s[4 * q] = v.x; s[4 * q + 1] = v.y; s[4 * q + 2] = v.z; s[4 * q + 3] = v.w;
-        };
-        xsum(0);
-        xsum(1);
-        // s[r] = logit(token t·32 + (r&3) + 8(r>>2) + 4hi, vocab v0 + c32)
-        float ds[16];
-        auto dsv = [&](int r) __attribute__((always_inline)) {
-            const int q = r >> 2, e = r & 3, tb = 8 * q + 4 * hi + e;  // token of the tile
-            const float gv = t * kLLRows + tb < nv ? sgg[q][e] : 0.0f;
-            const float pv = exp2_fast(fmaf(s[r], kLog2e, snl[q][e]));
-            ds[r] = gv * ((syy[q][e] == vcol ? 1.0f : 0.0f) - pv);
-        };
-#pragma unroll
-        for (int r = 0; r < 8; ++r) dsv(r);
-        const bf16x8_t db0 = pack8(ds);
-        bf16x8_t db1;
+        for (int r = 0; r < 4; ++r) dsv(1, r);
+        const bf16x8_t da = pack8(ds);  // A operand: slot 8g + j <- token t(g, j)
         __builtin_amdgcn_sched_barrier(0);
-        const char* ts_ = cur + sq * HS * 64;
+        // ---- dW phase: gap nb: tr reads nb+PFO | MFMA | the remaining DMA pieces
         constexpr int PFO = 4;
-        bf16x8_t tf[2 * OB];
+        bf16x8_t tf[DB];
 #pragma unroll
-        for (int i = 0; i < PFO; ++i) tf[i] = ll_tr_frag(ts_, LL, i / OB, i % OB);
+        for (int nb = 0; nb < PFO; ++nb) tf[nb] = tr_frag(cur, nb);
 #pragma unroll
-        for (int i = 0; i < 2 * OB; ++i) {
-            if (i + PFO < 2 * OB) tf[i + PFO] = ll_tr_frag(ts_, LL, (i + PFO) / OB, (i + PFO) % OB);
-            if (i == 0) {
-                xsum(2);
-                xsum(3);
-            }
-            if (i < 8) dsv(8 + i);
-            if (i == 7) db1 = pack8(ds + 8);  // before the first k-step-1 MFMA (gap OB >= 8)
-            const int b = i % OB;
-            D[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i < OB ? db0 : db1, tf[i], D[b], 0, 0, 0);
-            if ((KS + i) % 3 == 1 && (KS + i) / 3 < NI) issue_piece(t + 1, nxt, (KS + i) / 3, pa, pb);
+        for (int nb = 0; nb < DB; ++nb) {
+            if (nb + PFO < DB) tf[nb + PFO] = tr_frag(cur, nb + PFO);
+            D[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tf[nb], D[nb], 0, 0, 0);
+            const int gk = NG + nb;  // global gap index
+            if ((gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 1, nxt, gk >> 2, pa, pb);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
     for (int t = t0; t < t1; ++t) {
         __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t
         ll_lds_barrier();  // every wave's; and every wave is done with tile t-1
-        tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, xbuf, t);
+        tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, t);
     }
-    // D[b][r] = dW(vocab v0 + (r&3) + 8(r>>2) + 4hi, hidden sq·HS + 32b + c32)
+    // D[nb][r] = dW(vocab v0 + 4g + r, hidden 16nb + c)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int vr = grp * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi, v = vb * vpw + vr;
+    for (int r = 0; r < 4; ++r) {
+        const int vr = wave * 16 + 4 * g + r, v = vb * vpw + vr;
         if (part) {  // fp32 partial of this token split, summed by k_lmloss_dw_reduce
-            float* out = a.dwpart + (int64_t(j) * vpw + vr) * H + sq * HS + c32;
+            float* out = a.dwpart + (int64_t(j) * vpw + vr) * H + c;
 #pragma unroll
-            for (int b = 0; b < OB; ++b) out[32 * b] = D[b][r];
+            for (int nb = 0; nb < DB; ++nb) out[16 * nb] = D[nb][r];
         } else if (v < a.V) {
-            const int64_t o = int64_t(v) * a.lddw + sq * HS + c32;
+            const int64_t o = int64_t(v) * a.lddw + c;
             if (a.dw_dtype == TRLX_F32) {
                 float* out = static_cast<float*>(a.dw) + o;
 #pragma unroll
-                for (int b = 0; b < OB; ++b) out[32 * b] = D[b][r];
+                for (int nb = 0; nb < DB; ++nb) out[16 * nb] = D[nb][r];
             } else {
                 uint16_t* out = static_cast<uint16_t*>(a.dw) + o;
 #pragma unroll
-                for (int b = 0; b < OB; ++b) out[32 * b] = f2bf(D[b][r]);
+                for (int nb = 0; nb < DB; ++nb) out[16 * nb] = f2bf(D[nb][r]);
             }
         }
     }
@@ -1028,11 +1229,21 @@ __global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int
 // ------------------------------------------------------------------ host side
 static thread_local int g_ll_splits = 0;  // tuning "lmloss_splits" (0 = auto)
 static thread_local int g_ll_tsplit = 0;  // tuning "lmloss_dw_tsplit" (0 = auto)
+// tuning "lmloss_fwd": 0 auto (= 1), 1 the 32x32x16 pair form (ll_fwd_block), 2 the 16x16x32 form
+// (ll_fwd16_block: no exchange, but twice the LDS bytes per MFMA — measured 1123 vs ~1010 us
+// at C2, while the same trade won for dW, whose exchange and dS sat on the critical path)
+static thread_local int g_ll_fwd = 0;
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
     const bool sp = key && !__builtin_strcmp(key, "lmloss_splits");
     const bool ts = key && !__builtin_strcmp(key, "lmloss_dw_tsplit");
-    *handled = sp || ts;
+    const bool fw = key && !__builtin_strcmp(key, "lmloss_fwd");
+    *handled = sp || ts || fw;
+    if (fw) {
+        TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "lmloss_fwd: 0 auto (1), 1 32x32 pair form, 2 16x16 form");
+        g_ll_fwd = int(value);
+        return TRLX_OK;
+    }
     if (sp) {
         TRLX_REQUIRE(value >= 0 && value <= kLLMaxSplits, TRLX_ERR_ARG, "lmloss_splits: 0..%d", kLLMaxSplits);
         g_ll_splits = int(value);
@@ -1135,8 +1346,9 @@ template <class G>
 static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
     const int64_t ntb = (a.N + kLLTokBlock - 1) / kLLTokBlock;
     const unsigned grid = unsigned((ntb * a.nsplit + 7) / 8 * 8);
-    void (*first)(LmLossArgs) = k_lmloss_fwd<G, false>;
-    void (*restart)(LmLossArgs) = k_lmloss_fwd<G, true>;
+    const bool f16 = g_ll_fwd == 2;
+    void (*first)(LmLossArgs) = f16 ? k_lmloss_fwd<G, false, true> : k_lmloss_fwd<G, false, false>;
+    void (*restart)(LmLossArgs) = f16 ? k_lmloss_fwd<G, true, true> : k_lmloss_fwd<G, true, false>;
     hipLaunchKernelGGL(first, dim3(grid), dim3(G::kThreads), 0, s, a);
     const int rc = check_launch("k_lmloss_fwd");
     if (rc) return rc;
