@@ -8,6 +8,7 @@ trlx_lmhead_logprobs_fwd_saved (forward + combine) and trlx_lmhead_logprobs_bwd 
 at the C2 shape with HIP events, median of --iters.
 
   python tools/lmloss_ablate.py [--libs base,abl/lib_abl1.so,...] [--iters 20]
+  (LL_TUNE=key=value,... sets library tunings in each child; LL_STAMPS=1 with a -DLL_STAMP=1 build)
 """
 import argparse
 import json
@@ -25,6 +26,10 @@ def child(N, H, V, iters):
     import __graft_entry__
     P = __graft_entry__.load_package()
     L = P._lib
+    L.load()
+    for kv in filter(None, os.environ.get("LL_TUNE", "").split(",")):  # e.g. LL_TUNE=lmloss_dw_stage=1
+        k, v = kv.split("=")
+        L.set_tuning(k, int(v))
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     h = torch.randn(N, H, generator=g, device=dev).to(torch.bfloat16)
@@ -63,9 +68,9 @@ def child(N, H, V, iters):
         dm = buf[1 << 15:].reshape(-1, 8)
         dm = dm[dm[:, 6] > 0].astype(np.float64)
         if dm.size:
-            dper = dm[:, :5] / dm[:, 6:7]
+            dper = dm[:, :4] / dm[:, 6:7]
             out["dw_stamp_cycles_per_step"] = {n: round(float(v), 1) for n, v in zip(
-                ["wait_dma+barrier", "S_phase", "exchange", "dS_half", "dW_phase"], dper.mean(0))}
+                ["wait_dma+barrier", "S_phase", "dS_tail", "dW_phase"], dper.mean(0))}
         sm = buf[:1 << 15].reshape(-1, 8)
         sm = sm[sm[:, 6] > 0].astype(np.float64)
         per = sm[:, :6] / sm[:, 6:7]

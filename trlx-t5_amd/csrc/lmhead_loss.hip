@@ -890,23 +890,26 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
 }
 
 // ------------------------------------------------------------------ combine
-// One workgroup per compact token m, one thread per 4 hidden columns (H/4 threads: 192 / 128):
-// merge the vocab splits (fixed order), lse, lp, g, dh.
+// One workgroup per compact token m, one thread per 4 hidden columns (blockDim = H/4: 192 / 128):
+// merge the vocab splits (fixed order), lse, lp, g, dh.  Every load a thread needs is issued
+// before the one barrier (the cross-wave sum of the label logit): the splits' partial O and
+// (m, l) first — they depend on m only, splits past nsplit re-read the last one and are weighted
+// 0 — then the label row, and the PPO scalars, which every thread reads (same addresses) so
+// that each computes g itself and no second barrier broadcasts it.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
-    const int m = blockIdx.x, tid = threadIdx.x;
-    __shared__ float s_sc[kLLMaxSplits];
+    const int m = blockIdx.x, d4 = threadIdx.x;
     __shared__ float s_tok[4];
     int row = m;
     bool pad = false;
+    const int nv = a.rows ? *a.nrows : a.N;
     if (a.rows) {
         const int r = a.rows[m];
-        pad = m >= *a.nrows;
+        pad = m >= nv;
         row = pad ? ~r : r;
     }
-    const int H4 = a.H >> 2;
     if (pad) {  // a masked token (mask == 0): zero gradient, no logits needed (masked_row)
-        if (MODE == kLLPpo && tid == 0) {
+        if (MODE == kLLPpo && d4 == 0) {
             float vin[3];
             const PpoScalars p = ppo_scalars(a, row, vin, true);
             PolicyTerms pt;
@@ -915,113 +918,103 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
             token_record(a, row, pt, p, vin);
             if (a.coef || a.wstats) split_outputs(a, row, p);
         }
-        for (int d4 = tid; d4 < H4; d4 += blockDim.x) {
-            if (a.dh_dtype == TRLX_BF16)
-                reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.dh) + int64_t(row) * a.lddh)[d4] = make_uint2(0u, 0u);
-            else
-                reinterpret_cast<f32x4_t*>(static_cast<float*>(a.dh) + int64_t(row) * a.lddh)[d4] = f32x4_t{};
-        }
+        if (a.dh_dtype == TRLX_BF16)
+            reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.dh) + int64_t(row) * a.lddh)[d4] = make_uint2(0u, 0u);
+        else
+            reinterpret_cast<f32x4_t*>(static_cast<float*>(a.dh) + int64_t(row) * a.lddh)[d4] = f32x4_t{};
         return;
+    }
+    const int H4 = a.H >> 2;
+    f32x4_t op[kLLMaxSplits];
+    float2 ml[kLLMaxSplits];
+    int nsplit = 0;
+    if (MODE != kLLBwd) {
+        nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
+#pragma unroll
+        for (int s = 0; s < kLLMaxSplits; ++s) {
+            const int64_t sc = min(s, nsplit - 1);
+            op[s] = reinterpret_cast<const f32x4_t*>(a.opart + (sc * a.N + m) * a.H)[d4];
+            ml[s] = a.mlpart[sc * a.N + m];
+        }
     }
     const int64_t y = a.labels[int64_t(row) * a.lb];
     const bool yok = y >= 0 && y < a.V;
-    const uint16_t* wrow = a.w + (yok ? y : 0) * a.ldw;
-    float lse = 0.0f, L = 1.0f;
-    int nsplit = 0;
+    const uint2 wv = reinterpret_cast<const uint2*>(a.w + (yok ? y : 0) * a.ldw)[d4];
+    float lse = 0.0f, L = 1.0f, g = 0.0f;
+    f32x4_t e;
     if (MODE != kLLBwd) {
+        const uint2 hv = reinterpret_cast<const uint2*>(a.h + int64_t(row) * a.ldh)[d4];
+        float vin[3] = {0.0f, 0.0f, 0.0f};
+        PpoScalars p{};
+        if (MODE == kLLPpo) p = ppo_scalars(a, row, vin, true);
         // the label logit h·W[y] (fp32 products of the bf16 operands, fixed-order sums), kept
         // out of the forward's tile loop
-        float xl = 0.0f;
-        const uint16_t* hrow = a.h + int64_t(row) * a.ldh;
-        for (int d4 = tid; d4 < H4; d4 += blockDim.x) {
-            const uint2 hv = reinterpret_cast<const uint2*>(hrow)[d4];
-            const uint2 wv = reinterpret_cast<const uint2*>(wrow)[d4];
-            xl = fmaf(bf_lo(hv.x), bf_lo(wv.x), xl);
-            xl = fmaf(bf_hi(hv.x), bf_hi(wv.x), xl);
-            xl = fmaf(bf_lo(hv.y), bf_lo(wv.y), xl);
-            xl = fmaf(bf_hi(hv.y), bf_hi(wv.y), xl);
-        }
+        float xl = bf_lo(hv.x) * bf_lo(wv.x);
+        xl = fmaf(bf_hi(hv.x), bf_hi(wv.x), xl);
+        xl = fmaf(bf_lo(hv.y), bf_lo(wv.y), xl);
+        xl = fmaf(bf_hi(hv.y), bf_hi(wv.y), xl);
         for (int off = 32; off > 0; off >>= 1) xl += __shfl_xor(xl, off);
-        if ((tid & 63) == 0) s_tok[tid >> 6] = xl;
+        if ((d4 & 63) == 0) s_tok[d4 >> 6] = xl;
         __syncthreads();
         float xlab = s_tok[0];  // the waves' sums in wave order
-        for (int w = 1; w < int(blockDim.x >> 6); ++w) xlab += s_tok[w];
-        __syncthreads();  // s_tok is reused below
+        for (int w = 1; w < (H4 + 63) / 64; ++w) xlab += s_tok[w];
         float M = -INFINITY;
-        const int nv = a.rows ? *a.nrows : a.N;
-        nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
-        for (int s = 0; s < nsplit; ++s) M = fmaxf(M, a.mlpart[int64_t(s) * a.N + m].x);
+#pragma unroll
+        for (int s = 0; s < kLLMaxSplits; ++s)
+            if (s < nsplit) M = fmaxf(M, ml[s].x);
         L = 0.0f;
-        for (int s = 0; s < nsplit; ++s) {
-            const float2 p = a.mlpart[int64_t(s) * a.N + m];
-            const float sc = p.x == -INFINITY ? 0.0f : exp2_fast((p.x - M) * kLog2e);
-            L += p.y * sc;
-            if (tid == s) s_sc[s] = sc;
+        e = f32x4_t{};
+#pragma unroll
+        for (int s = 0; s < kLLMaxSplits; ++s) {
+            if (s >= nsplit) break;
+            const float sc = ml[s].x == -INFINITY ? 0.0f : exp2_fast((ml[s].x - M) * kLog2e);
+            L += ml[s].y * sc;
+            e += sc * op[s];
         }
         const float lsum = logf(L);
         lse = M + lsum;
-        if (tid == 0) {
-            const float lp = yok ? (xlab - M) - lsum : NAN;  // the reference's order, as in the rows
-            float g = 0.0f;
-            if (MODE == kLLPpo) {
-                float vin[3];
-                const PpoScalars p = ppo_scalars(a, row, vin, true);
-                PolicyTerms pt;
-                g = ppo_policy_dlp(lp, p.olp, p.A, p.m, p.inv_msum, a.cliprange, pt);
+        e *= 1.0f / L;
+        const float lp = yok ? (xlab - M) - lsum : NAN;  // the reference's order, as in the rows
+        if (MODE == kLLPpo) {
+            PolicyTerms pt;
+            g = ppo_policy_dlp(lp, p.olp, p.A, p.m, p.inv_msum, a.cliprange, pt);
+            if (d4 == 0) {
                 const bool masked = p.m == 0.0f;
                 a.lp_out[row] = masked ? 0.0f : lp;
                 if (masked) ppo_policy_dlp(0.0f, p.olp, p.A, p.m, p.inv_msum, a.cliprange, pt);
                 token_record(a, row, pt, p, vin);
                 if (a.coef || a.wstats) split_outputs(a, row, p);
                 a.gbuf[m] = g;
-            } else {  // kLLFwd
-                st_any(a.lp, a.lp_dtype, row, lp);
-                if (a.lse_io) a.lse_io[row] = lse;
             }
-            a.nlse[m] = -lse * kLog2e;
-            a.ybuf[m] = yok ? int(y) : -1;
-            s_tok[0] = g;
+        } else if (d4 == 0) {  // kLLFwd
+            st_any(a.lp, a.lp_dtype, row, lp);
+            if (a.lse_io) a.lse_io[row] = lse;
         }
     } else {  // kLLBwd: lse from the forward, g = the caller's d loss / d lp
-        if (tid == 0) {
-            lse = a.lse_io[row];
-            const float g = ld_any(a.gin, a.gin_dtype, row);
-            a.gbuf[m] = g;
-            a.nlse[m] = -lse * kLog2e;
-            a.ybuf[m] = yok ? int(y) : -1;
-            s_tok[0] = g;
-        }
+        e = reinterpret_cast<const f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4];
+        lse = a.lse_io[row];
+        g = ld_any(a.gin, a.gin_dtype, row);
+        if (d4 == 0) a.gbuf[m] = g;
     }
-    __syncthreads();
-    const float g = s_tok[0];
-    const float invL = 1.0f / L;
-    for (int d4 = tid; d4 < H4; d4 += blockDim.x) {
-        f32x4_t e;
-        if (MODE == kLLBwd) {
-            e = reinterpret_cast<const f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4];
-        } else {
-            e = f32x4_t{};
-            for (int s = 0; s < nsplit; ++s)
-                e += s_sc[s] * reinterpret_cast<const f32x4_t*>(a.opart + (int64_t(s) * a.N + m) * a.H)[d4];
-            e *= invL;
-        }
-        if (MODE == kLLFwd) {
-            reinterpret_cast<f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4] = e;
-            continue;
-        }
-        const uint2 wv = reinterpret_cast<const uint2*>(wrow)[d4];
-        f32x4_t d;
-        d.x = g * (bf_lo(wv.x) - e.x);
-        d.y = g * (bf_hi(wv.x) - e.y);
-        d.z = g * (bf_lo(wv.y) - e.z);
-        d.w = g * (bf_hi(wv.y) - e.w);
-        if (!yok) d = f32x4_t{NAN, NAN, NAN, NAN};
-        if (a.dh_dtype == TRLX_BF16)
-            reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.dh) + int64_t(row) * a.lddh)[d4] =
-                make_uint2(pack_bf2(d.x, d.y), pack_bf2(d.z, d.w));
-        else
-            reinterpret_cast<f32x4_t*>(static_cast<float*>(a.dh) + int64_t(row) * a.lddh)[d4] = d;
+    if (d4 == 0) {
+        a.nlse[m] = -lse * kLog2e;
+        a.ybuf[m] = yok ? int(y) : -1;
     }
+    if (MODE == kLLFwd) {
+        reinterpret_cast<f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4] = e;
+        return;
+    }
+    f32x4_t d;
+    d.x = g * (bf_lo(wv.x) - e.x);
+    d.y = g * (bf_hi(wv.x) - e.y);
+    d.z = g * (bf_lo(wv.y) - e.z);
+    d.w = g * (bf_hi(wv.y) - e.w);
+    if (!yok) d = f32x4_t{NAN, NAN, NAN, NAN};
+    if (a.dh_dtype == TRLX_BF16)
+        reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.dh) + int64_t(row) * a.lddh)[d4] =
+            make_uint2(pack_bf2(d.x, d.y), pack_bf2(d.z, d.w));
+    else
+        reinterpret_cast<f32x4_t*>(static_cast<float*>(a.dh) + int64_t(row) * a.lddh)[d4] = d;
 }
 
 // ------------------------------------------------------------------ dW
@@ -1041,12 +1034,18 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
 // Twice the h bytes read from LDS per MFMA of the 32x32 pair form (each wave reads the whole
 // tile, for S and for dW), in exchange for no group sum, no barrier inside the tile and the
 // dS of one block computed beside the other block's MFMAs.
-template <class G>
+// STAGE: tile t+1 fetched by plain buffer loads into registers in the S phase and written to
+// LDS (ds_write_b128, the same image) in the dW phase, instead of LDS-DMA pieces, whose issue
+// costs their wave 60-185 cycles each among LDS reads (MI355X_MICROARCH.md, LDS-DMA issue row).
+// PIPE: a 3-stage ring and a software-pipelined step — Sᵀ(t+1) from the next stage while the
+// dS of tile t (its Sᵀ finished the step before) is computed in the first gaps, then dW(t).
+template <class G, bool STAGE, bool PIPE>
 __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
     constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI;
     constexpr int kStage = G::kStage + 768;  // h tile + {-lse·log2e, g, y} x 64 lanes
     static_assert(G::kWaves == 4, "dW: four 16-row waves per 64-row workgroup");
-    __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
+    static_assert(!PIPE || 3 * kStage <= 163840, "dW: three stages must fit the LDS");
+    __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 3 : 2) * kStage];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, c = lane & 15;
@@ -1100,6 +1099,12 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
                                                  t < t1 ? off : int(0x7ffff000), 0, 0, 0);
     };
+    // STAGE: piece k of tile t into registers (past the last tile: the resource's zero fill)
+    auto load_piece = [&](int t, int k, int ra, int rbw) __attribute__((always_inline)) {
+        const int i = wave + G::kWaves * k;
+        const int off = ll_piece_src(i, (((i & 7) == (wave & 7)) ? ra : rbw) * int(a.ldh) * 2, lane);
+        return __builtin_amdgcn_raw_buffer_load_b128(rh, t < t1 ? off : int(0x7ffff000), 0, 0);
+    };
     // token scalars of tile t (wave 0): {-lse·log2e, g, y} of token min(t·32 + l&31, nv-1) in
     // lanes l and l+32 alike
     auto issue_scalars = [&](int t, char* slot) __attribute__((always_inline)) {
@@ -1114,9 +1119,9 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
     f32x4_t D[DB];  // dW[v0 + 4g + r][16nb + c]
 #pragma unroll
     for (int nb = 0; nb < DB; ++nb) D[nb] = f32x4_t{};
-    if (t0 < t1) {
+    if (!PIPE && t0 < t1) {
 #pragma unroll
-        for (int k = 0; k < NI; ++k) issue_piece(t0, smem, k, rowA, rowB);
+        for (int k = 0; k < NI; ++k) issue_piece(t0, smem, k, rowA, rowB);  // (both forms)
         if (wave == 0) issue_scalars(t0, smem);
     }
     constexpr int NG = 2 * KS;  // S-phase gaps
@@ -1124,7 +1129,12 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
     // tile t+2's rows: loaded unconditionally (a zero-size resource without compaction), picked
     // at the next tile — a load under a branch made hipcc wait for it at the branch's join
     const __amdgpu_buffer_rsrc_t rrows = make_rsrc(a.rows, a.rows ? uint32_t(a.N) * 4u : 0u);
+#if LL_STAMP
+    unsigned long long stamp[8] = {};
+#endif
     auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, int t) __attribute__((always_inline)) {
+        unsigned long long ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0;
+        LL_TS(ts1);
         const int pa = a.rows ? nrowA : min((t + 1) * kLLRows + rA, nv - 1);  // tile t+1's rows
         const int pb = a.rows ? nrowB : min((t + 1) * kLLRows + rB, nv - 1);
         nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 2) * kLLRows + rA, nv - 1) * 4, 0, 0);
@@ -1134,6 +1144,7 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
         int4 syy[2];
         f32x4_t sacc[2] = {f32x4_t{}, f32x4_t{}};
         float ds[8];
+        vec4u stg[STAGE ? NI : 1];
         auto dsv = [&](int mb, int r) __attribute__((always_inline)) {
             const int tb = 16 * mb + 4 * g + r;  // token of the tile
             const float gv = t * kLLRows + tb < nv ? sgg[mb][r] : 0.0f;
@@ -1151,7 +1162,12 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
             if (k + PF < NG) af[k + PF] = row_frag(cur, (k + PF) / KS, (k + PF) % KS);
             const int mb = k / KS, ks = k % KS;
             sacc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], wf[ks], sacc[mb], 0, 0, 0);
-            if ((k & 3) == 1 && (k >> 2) < NI) issue_piece(t + 1, nxt, k >> 2, pa, pb);
+            if ((k & 3) == 1 && (k >> 2) < NI) {
+                if (STAGE)
+                    stg[k >> 2] = load_piece(t + 1, k >> 2, pa, pb);
+                else
+                    issue_piece(t + 1, nxt, k >> 2, pa, pb);
+            }
             if (k >= 2 && k < 8) {
                 const int n = k - 2, b2 = n & 1;
                 if (n < 2) snl[b2] = *reinterpret_cast<const f32x4_t*>(scb + 4 * (16 * b2 + 4 * g));
@@ -1161,11 +1177,13 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
             if (k >= KS + 4 && k < KS + 8) dsv(0, k - KS - 4);  // block 0's S is final (+latency)
             __builtin_amdgcn_sched_barrier(0);
         }
+        LL_TS(ts2);
         if (wave == 0) issue_scalars(t + 1, nxt);
 #pragma unroll
         for (int r = 0; r < 4; ++r) dsv(1, r);
         const bf16x8_t da = pack8(ds);  // A operand: slot 8g + j <- token t(g, j)
         __builtin_amdgcn_sched_barrier(0);
+        LL_TS(ts3);
         // ---- dW phase: gap nb: tr reads nb+PFO | MFMA | the remaining DMA pieces
         constexpr int PFO = 4;
         bf16x8_t tf[DB];
@@ -1176,15 +1194,158 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
             if (nb + PFO < DB) tf[nb + PFO] = tr_frag(cur, nb + PFO);
             D[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tf[nb], D[nb], 0, 0, 0);
             const int gk = NG + nb;  // global gap index
-            if ((gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 1, nxt, gk >> 2, pa, pb);
+            if (!STAGE && (gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 1, nxt, gk >> 2, pa, pb);
+            if (STAGE && (nb & 3) == 1 && (nb >> 2) < NI) {
+                const int i = wave + G::kWaves * (nb >> 2);
+                *reinterpret_cast<vec4u*>(nxt + i * 1024 + 16 * lane) = stg[nb >> 2];
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
+        LL_TS(ts4);
+#if LL_STAMP
+        stamp[1] += ts2 - ts1;
+        stamp[2] += ts3 - ts2;
+        stamp[3] += ts4 - ts3;
+        stamp[6] += 1;
+#endif
+        (void)ts1, (void)ts2, (void)ts3, (void)ts4;
     };
-    for (int t = t0; t < t1; ++t) {
-        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t
-        ll_lds_barrier();  // every wave's; and every wave is done with tile t-1
-        tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, t);
+    if (!PIPE) {
+        for (int t = t0; t < t1; ++t) {
+            unsigned long long ts0 = 0, ts1 = 0;
+            LL_TS(ts0);
+            __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t
+            ll_lds_barrier();  // every wave's; and every wave is done with tile t-1
+            LL_TS(ts1);
+#if LL_STAMP
+            stamp[0] += ts1 - ts0;
+#endif
+            (void)ts0, (void)ts1;
+            tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, t);
+        }
+    } else if (t0 < t1) {
+        // ---- PIPE: carried between steps — Sᵀ of tile t (sacc) and its token scalars
+        f32x4_t sacc[2] = {f32x4_t{}, f32x4_t{}};
+        f32x4_t snl[2], sgg[2];
+        int4 syy[2];
+        float ds[8];
+        auto dsv = [&](int t, int mb, int r) __attribute__((always_inline)) {
+            const int tb = 16 * mb + 4 * g + r;
+            const float gv = t * kLLRows + tb < nv ? sgg[mb][r] : 0.0f;
+            const float pv = exp2_fast(fmaf(sacc[mb][r], kLog2e, snl[mb][r]));
+            ds[4 * mb + r] = gv * ((syy[mb][r] == vcol ? 1.0f : 0.0f) - pv);
+        };
+        auto read_scalars = [&](const char* slot, int n) __attribute__((always_inline)) {
+            const char* scb = slot + G::kStage;
+            const int b2 = n & 1;
+            if (n < 2) snl[b2] = *reinterpret_cast<const f32x4_t*>(scb + 4 * (16 * b2 + 4 * g));
+            else if (n < 4) sgg[b2] = *reinterpret_cast<const f32x4_t*>(scb + 256 + 4 * (16 * b2 + 4 * g));
+            else syy[b2] = *reinterpret_cast<const int4*>(scb + 512 + 4 * (16 * b2 + 4 * g));
+        };
+        auto dw_phase = [&](const char* __restrict__ cur, char* __restrict__ fut, const bf16x8_t& da,
+                            const vec4u* stg) __attribute__((always_inline)) {
+            constexpr int PFO = 4;
+            bf16x8_t tf[DB];
+#pragma unroll
+            for (int nb = 0; nb < PFO; ++nb) tf[nb] = tr_frag(cur, nb);
+#pragma unroll
+            for (int nb = 0; nb < DB; ++nb) {
+                if (nb + PFO < DB) tf[nb + PFO] = tr_frag(cur, nb + PFO);
+                D[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tf[nb], D[nb], 0, 0, 0);
+                if (STAGE && stg && (nb & 3) == 1 && (nb >> 2) < NI) {
+                    const int i = wave + G::kWaves * (nb >> 2);
+                    *reinterpret_cast<vec4u*>(fut + i * 1024 + 16 * lane) = stg[nb >> 2];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        char* c0 = smem;
+        char* c1 = smem + kStage;
+        char* c2 = smem + 2 * kStage;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) issue_piece(t0, c0, k, rowA, rowB);
+        if (wave == 0) issue_scalars(t0, c0);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) issue_piece(t0 + 1, c1, k, nrowA, nrowB);
+        if (wave == 0) issue_scalars(t0 + 1, c1);
+        nrowA = tok_row((t0 + 2) * kLLRows + rA);
+        nrowB = tok_row((t0 + 2) * kLLRows + rB);
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));
+        ll_lds_barrier();
+#pragma unroll
+        for (int k = 0; k < NG; ++k)
+            sacc[k / KS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(c0, k / KS, k % KS), wf[k % KS],
+                                                                   sacc[k / KS], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < 6; ++n) read_scalars(c0, n);
+        // step t: cur (tile t), nx (tile t+1, landed), fut (tile t+2); the regions as
+        // __restrict__ parameters (alias scopes: no DMA wait before the reads of nx)
+        auto step = [&](const char* __restrict__ cur, const char* __restrict__ nx, char* __restrict__ fut,
+                        int t) __attribute__((always_inline)) {
+            unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
+            LL_TS(ts0);
+            __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t+1
+            ll_lds_barrier();  // every wave's; and every wave is done with tile t-1 (= c2)
+            LL_TS(ts1);
+            const int pa = a.rows ? nrowA : min((t + 2) * kLLRows + rA, nv - 1);  // tile t+2's rows
+            const int pb = a.rows ? nrowB : min((t + 2) * kLLRows + rB, nv - 1);
+            nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rA, nv - 1) * 4, 0, 0);
+            nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rB, nv - 1) * 4, 0, 0);
+            vec4u stg[STAGE ? NI : 1];
+            f32x4_t sn[2] = {f32x4_t{}, f32x4_t{}};
+            bf16x8_t da;
+            // ---- phase 1, gap k: row read k+PF of tile t+1 | MFMA k of Sᵀ(t+1) | piece of
+            // tile t+2 every 4th gap | dS(t) in the even gaps 0..14 | tile t+1's scalars 18..23
+            constexpr int PF = 4;
+            bf16x8_t af[NG];
+#pragma unroll
+            for (int k = 0; k < PF; ++k) af[k] = row_frag(nx, k / KS, k % KS);
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                if (k + PF < NG) af[k + PF] = row_frag(nx, (k + PF) / KS, (k + PF) % KS);
+                sn[k / KS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], wf[k % KS], sn[k / KS], 0, 0, 0);
+                if ((k & 3) == 1 && (k >> 2) < NI) {
+                    if (STAGE)
+                        stg[k >> 2] = load_piece(t + 2, k >> 2, pa, pb);
+                    else
+                        issue_piece(t + 2, fut, k >> 2, pa, pb);
+                }
+                if (k < 16 && (k & 1) == 0) dsv(t, k >> 3, (k >> 1) & 3);
+                if (k == 16) da = pack8(ds);  // A operand: slot 8g + j <- token t(g, j)
+                if (k >= 18 && k < 24) read_scalars(nx, k - 18);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (wave == 0) issue_scalars(t + 2, fut);
+            LL_TS(ts2);
+            dw_phase(cur, fut, da, STAGE ? stg : nullptr);
+            LL_TS(ts3);
+#if LL_STAMP
+            stamp[0] += ts1 - ts0;
+            stamp[1] += ts2 - ts1;
+            stamp[3] += ts3 - ts2;
+            stamp[6] += 1;
+#endif
+            (void)ts0, (void)ts1, (void)ts2, (void)ts3;
+            sacc[0] = sn[0];
+            sacc[1] = sn[1];
+        };
+        for (int t = t0; t + 1 < t1; ++t) {
+            step(c0, c1, c2, t);
+            char* cc = c0;
+            c0 = c1;
+            c1 = c2;
+            c2 = cc;
+        }
+        // the last tile: its dS and dW
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dsv(t1 - 1, q >> 2, q & 3);
+        const bf16x8_t da = pack8(ds);
+        dw_phase(c0, c2, da, nullptr);
     }
+#if LL_STAMP
+    if (lane == 0 && blockIdx.x * 4 + wave < (1 << 12))
+        for (int k = 0; k < 8; ++k) g_ll_stamps[(1 << 15) + (blockIdx.x * 4 + wave) * 8 + k] = stamp[k];
+#endif
     // D[nb][r] = dW(vocab v0 + 4g + r, hidden 16nb + c)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1233,12 +1394,20 @@ static thread_local int g_ll_tsplit = 0;  // tuning "lmloss_dw_tsplit" (0 = auto
 // (ll_fwd16_block: no exchange, but twice the LDS bytes per MFMA — measured 1123 vs ~1010 us
 // at C2, while the same trade won for dW, whose exchange and dS sat on the critical path)
 static thread_local int g_ll_fwd = 0;
+static thread_local int g_ll_dw_stage = 0;  // tuning "lmloss_dw_stage": bit 0 register-staged, bit 1 pipelined
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
     const bool sp = key && !__builtin_strcmp(key, "lmloss_splits");
     const bool ts = key && !__builtin_strcmp(key, "lmloss_dw_tsplit");
     const bool fw = key && !__builtin_strcmp(key, "lmloss_fwd");
-    *handled = sp || ts || fw;
+    const bool dst = key && !__builtin_strcmp(key, "lmloss_dw_stage");
+    *handled = sp || ts || fw || dst;
+    if (dst) {
+        TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG,
+                     "lmloss_dw_stage: 0 LDS-DMA, 1 register-staged, 2 pipelined (3 stages), 3 both");
+        g_ll_dw_stage = int(value);
+        return TRLX_OK;
+    }
     if (fw) {
         TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "lmloss_fwd: 0 auto (1), 1 32x32 pair form, 2 16x16 form");
         g_ll_fwd = int(value);
@@ -1357,7 +1526,11 @@ static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
 }
 template <class G>
 static int ll_launch_dw(const LmLossArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lmloss_dw<G>, dim3(unsigned(a.dw_full + a.dw_nblk * a.tsplit)), dim3(G::kThreads), 0, s, a);
+    void (*k)(LmLossArgs) = g_ll_dw_stage == 1   ? k_lmloss_dw<G, true, false>
+                            : g_ll_dw_stage == 2 ? k_lmloss_dw<G, false, true>
+                            : g_ll_dw_stage == 3 ? k_lmloss_dw<G, true, true>
+                                                 : k_lmloss_dw<G, false, false>;
+    hipLaunchKernelGGL(k, dim3(unsigned(a.dw_full + a.dw_nblk * a.tsplit)), dim3(G::kThreads), 0, s, a);
     return check_launch("k_lmloss_dw");
 }
 static int ll_fwd(const LmLossArgs& a, hipStream_t s) {
