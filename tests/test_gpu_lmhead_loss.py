@@ -335,34 +335,3 @@ def test_lm_head_logprobs_forward_forms(form, N, H, V):
     finally:
         P._lib.set_tuning("lmloss_fwd", 0)
 
-
-@pytest.mark.parametrize("stage", [1, 2, 3])
-@pytest.mark.parametrize("N,H,V,tsplit", [(200, 768, 7000, 0), (200, 768, 7000, 16), (70, 512, 33, 0),
-                                          (300, 768, 50257, 0), (33, 768, 5000, 3)])
-def test_lm_head_dw_forms(stage, N, H, V, tsplit):
-    """The dW kernel's forms (tuning lmloss_dw_stage: bit 0 register-staged tiles instead of
-    LDS-DMA, bit 1 the 3-stage software-pipelined step) do the same arithmetic in the same
-    order: dW bit-identical to the default form, and within the fp64 tolerance.  Token splits
-    of 0 and 1 tiles (tsplit 16 over 7 tiles) and single-tile blocks included."""
-    h, w, y = _operands(N, H, V, N + stage)
-    gout = torch.randn(N, generator=torch.Generator().manual_seed(stage))
-
-    def run():
-        hg = h.to(DEV).requires_grad_(True)
-        wg = w.to(DEV).requires_grad_(True)
-        lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32)
-        (lp * gout.to(DEV)).sum().backward()
-        torch.cuda.synchronize()
-        return hg.grad, wg.grad
-
-    P._lib.set_tuning("lmloss_dw_tsplit", tsplit)
-    try:
-        base = run()
-        P._lib.set_tuning("lmloss_dw_stage", stage)
-        got = run()
-    finally:
-        P._lib.set_tuning("lmloss_dw_stage", 0)
-        P._lib.set_tuning("lmloss_dw_tsplit", 0)
-    assert torch.equal(got[1], base[1]) and torch.equal(got[0], base[0])
-    _, dh64, dw64 = _fp64_grads(h, w, y, gout)
-    assert _rel(got[0], dh64) < 1e-2 and _rel(got[1], dw64) < 1e-2

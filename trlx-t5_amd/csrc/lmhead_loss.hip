@@ -92,9 +92,8 @@ struct LmLossArgs {
     int nsplit_fixed;
     float* opart;    // [nsplit][N][H] partial O (compact token index)
     float2* mlpart;  // [nsplit][N] partial (m, l)
-    float* nlse;     // [N] -lse·log2e (compact; read by the dW kernel)
-    float* gbuf;     // [N] d loss / d lp (compact)
-    int* ybuf;       // [N] label (compact)
+    float* trec;     // [N][4] token records {-lse·log2e, d loss / d lp, label bits, 0} (compact;
+                     // one 16-B LDS-DMA per lane in the dW kernel)
     int* flags;      // [forward grid][waves] 1 = the wave's fixed offset overflowed (k_lmloss_fwd)
     float* ebuf;     // kLLFwd: E = O / l written here; kLLBwd: read ([N, H], token rows)
     float* lse_io;   // kLLFwd: lse out; kLLBwd: lse in (token rows); may be NULL in kLLPpo
@@ -984,7 +983,6 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
                 if (masked) ppo_policy_dlp(0.0f, p.olp, p.A, p.m, p.inv_msum, a.cliprange, pt);
                 token_record(a, row, pt, p, vin);
                 if (a.coef || a.wstats) split_outputs(a, row, p);
-                a.gbuf[m] = g;
             }
         } else if (d4 == 0) {  // kLLFwd
             st_any(a.lp, a.lp_dtype, row, lp);
@@ -994,11 +992,10 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
         e = reinterpret_cast<const f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4];
         lse = a.lse_io[row];
         g = ld_any(a.gin, a.gin_dtype, row);
-        if (d4 == 0) a.gbuf[m] = g;
     }
     if (d4 == 0) {
-        a.nlse[m] = -lse * kLog2e;
-        a.ybuf[m] = yok ? int(y) : -1;
+        const f32x4_t rec = {-lse * kLog2e, g, __int_as_float(yok ? int(y) : -1), 0.0f};
+        reinterpret_cast<f32x4_t*>(a.trec)[m] = rec;
     }
     if (MODE == kLLFwd) {
         reinterpret_cast<f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4] = e;
@@ -1034,18 +1031,15 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
 // Twice the h bytes read from LDS per MFMA of the 32x32 pair form (each wave reads the whole
 // tile, for S and for dW), in exchange for no group sum, no barrier inside the tile and the
 // dS of one block computed beside the other block's MFMAs.
-// STAGE: tile t+1 fetched by plain buffer loads into registers in the S phase and written to
-// LDS (ds_write_b128, the same image) in the dW phase, instead of LDS-DMA pieces, whose issue
-// costs their wave 60-185 cycles each among LDS reads (MI355X_MICROARCH.md, LDS-DMA issue row).
-// PIPE: a 3-stage ring and a software-pipelined step — Sᵀ(t+1) from the next stage while the
-// dS of tile t (its Sᵀ finished the step before) is computed in the first gaps, then dW(t).
-template <class G, bool STAGE, bool PIPE>
+// Two forms measured slower at C2 (round 4, profiles/r04s_*): tiles staged through registers
+// (buffer_load + ds_write_b128 instead of LDS-DMA: the dW phase 1,552 -> 2,018 cycles a tile)
+// and a 3-stage software-pipelined step (dS(t) beside Sᵀ(t+1): the dS work moved, not hidden).
+template <class G>
 __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
     constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI;
-    constexpr int kStage = G::kStage + 768;  // h tile + {-lse·log2e, g, y} x 64 lanes
+    constexpr int kStage = G::kStage + 1024;  // h tile + the token records (16 B x 64 lanes)
     static_assert(G::kWaves == 4, "dW: four 16-row waves per 64-row workgroup");
-    static_assert(!PIPE || 3 * kStage <= 163840, "dW: three stages must fit the LDS");
-    __shared__ __attribute__((aligned(16))) char smem[(PIPE ? 3 : 2) * kStage];
+    __shared__ __attribute__((aligned(16))) char smem[2 * kStage];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, c = lane & 15;
@@ -1079,8 +1073,10 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
         return ll16_row_frag(tile, rb, mb, ks);
     };
     auto tr_frag = [&](const char* tile, int nb) __attribute__((always_inline)) { return ll16_tr_frag(tile, trb, nb); };
-    // the tile rows this lane's DMA pieces fetch (pieces i = wave + 4k: two distinct rows)
-    auto tok_row = [&](int m) { const int mc = min(m, nv - 1); return a.rows ? a.rows[mc] : mc; };
+    // the tile rows this lane's DMA pieces fetch (pieces i = wave + 4k: two distinct rows); row
+    // N (out of the resource) past the live tokens: those rows are zero-filled, and so are their
+    // records (g = 0, S = 0)
+    auto tok_row = [&](int m) { return m < nv ? (a.rows ? a.rows[m] : m) : a.N; };
     int rowA = 0, rowB = 0, nrowA = 0, nrowB = 0;
     const int rA = ll_piece_row(wave, lane), rB = ll_piece_row(wave + G::kWaves, lane);
     if (t0 < t1) {
@@ -1090,38 +1086,30 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
         nrowB = tok_row((t0 + 1) * kLLRows + rB);
     }
     const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.h, uint32_t(int64_t(a.N) * a.ldh * 2));
-    const __amdgpu_buffer_rsrc_t rnl = make_rsrc(a.nlse, uint32_t(a.N) * 4u);
-    const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gbuf, uint32_t(a.N) * 4u);
-    const __amdgpu_buffer_rsrc_t ry = make_rsrc(a.ybuf, uint32_t(a.N) * 4u);
+    const __amdgpu_buffer_rsrc_t rrec = make_rsrc(a.trec, uint32_t(a.N) * 16u);
     auto issue_piece = [&](int t, char* slot, int k, int ra, int rbw) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
-        const int off = ll_piece_src(i, (((i & 7) == (wave & 7)) ? ra : rbw) * int(a.ldh) * 2, lane);
+        // 24-bit multiply (rows < 2^24, row bytes < 2^24): a 32-bit product here became a
+        // v_mad_u64_u32 whose unused high addend register was a pending load's destination
+        const int rbytes = int(__umul24(uint32_t(((i & 7) == (wave & 7)) ? ra : rbw), uint32_t(a.ldh) * 2u));
+        const int off = ll_piece_src(i, rbytes, lane);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
                                                  t < t1 ? off : int(0x7ffff000), 0, 0, 0);
     };
-    // STAGE: piece k of tile t into registers (past the last tile: the resource's zero fill)
-    auto load_piece = [&](int t, int k, int ra, int rbw) __attribute__((always_inline)) {
-        const int i = wave + G::kWaves * k;
-        const int off = ll_piece_src(i, (((i & 7) == (wave & 7)) ? ra : rbw) * int(a.ldh) * 2, lane);
-        return __builtin_amdgcn_raw_buffer_load_b128(rh, t < t1 ? off : int(0x7ffff000), 0, 0);
-    };
-    // token scalars of tile t (wave 0): {-lse·log2e, g, y} of token min(t·32 + l&31, nv-1) in
-    // lanes l and l+32 alike
+    // the token records of tile t (wave 0): token t·32 + (l & 31)'s 16 B at byte 16·l (lanes l
+    // and l+32 alike); zero past the live tokens — with their zero h rows, dS = 0 exactly
+    // (S = 0, p = 2^0, g = 0) and no per-value test
     auto issue_scalars = [&](int t, char* slot) __attribute__((always_inline)) {
-        const int mi = (t < t1 ? min(t * kLLRows + (lane & 31), nv - 1) : 0x1fffffff) * 4;
-        char* sc = slot + G::kStage;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rnl, (__attribute__((address_space(3))) void*)sc, 4, mi, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (__attribute__((address_space(3))) void*)(sc + 256), 4, mi, 0, 0,
-                                                 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (__attribute__((address_space(3))) void*)(sc + 512), 4, mi, 0, 0,
-                                                 0);
+        const int m = t * kLLRows + (lane & 31);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rrec, (__attribute__((address_space(3))) void*)(slot + G::kStage),
+                                                 16, t < t1 && m < nv ? m * 16 : int(0x7ffffff0), 0, 0, 0);
     };
     f32x4_t D[DB];  // dW[v0 + 4g + r][16nb + c]
 #pragma unroll
     for (int nb = 0; nb < DB; ++nb) D[nb] = f32x4_t{};
-    if (!PIPE && t0 < t1) {
+    if (t0 < t1) {
 #pragma unroll
-        for (int k = 0; k < NI; ++k) issue_piece(t0, smem, k, rowA, rowB);  // (both forms)
+        for (int k = 0; k < NI; ++k) issue_piece(t0, smem, k, rowA, rowB);
         if (wave == 0) issue_scalars(t0, smem);
     }
     constexpr int NG = 2 * KS;  // S-phase gaps
@@ -1135,8 +1123,9 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
     auto tile = [&](const char* __restrict__ cur, char* __restrict__ nxt, int t) __attribute__((always_inline)) {
         unsigned long long ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0;
         LL_TS(ts1);
-        const int pa = a.rows ? nrowA : min((t + 1) * kLLRows + rA, nv - 1);  // tile t+1's rows
-        const int pb = a.rows ? nrowB : min((t + 1) * kLLRows + rB, nv - 1);
+        const int ma = (t + 1) * kLLRows + rA, mb1 = (t + 1) * kLLRows + rB;  // tile t+1's rows
+        const int pa = ma < nv ? (a.rows ? nrowA : ma) : a.N;
+        const int pb = mb1 < nv ? (a.rows ? nrowB : mb1) : a.N;
         nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 2) * kLLRows + rA, nv - 1) * 4, 0, 0);
         nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 2) * kLLRows + rB, nv - 1) * 4, 0, 0);
         const char* scb = cur + G::kStage;
@@ -1144,15 +1133,14 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
         int4 syy[2];
         f32x4_t sacc[2] = {f32x4_t{}, f32x4_t{}};
         float ds[8];
-        vec4u stg[STAGE ? NI : 1];
+        // dS = g·(1[y = v] − p) as g − g·p / −g·p (one fma; g = 0 past the live tokens)
         auto dsv = [&](int mb, int r) __attribute__((always_inline)) {
-            const int tb = 16 * mb + 4 * g + r;  // token of the tile
-            const float gv = t * kLLRows + tb < nv ? sgg[mb][r] : 0.0f;
+            const float gv = sgg[mb][r];
             const float pv = exp2_fast(fmaf(sacc[mb][r], kLog2e, snl[mb][r]));
-            ds[4 * mb + r] = gv * ((syy[mb][r] == vcol ? 1.0f : 0.0f) - pv);
+            ds[4 * mb + r] = fmaf(-gv, pv, syy[mb][r] == vcol ? gv : 0.0f);
         };
         // ---- S phase: gap k = 24mb + ks (mb-major): row read k+PF | MFMA | DMA piece every
-        // 4th gap | the tile's scalars read in gaps 2..7 | dS of block 0 in the gaps of block 1
+        // 4th gap | the tile's records read in gaps 2..9 | dS of block 0 in the gaps of block 1
         constexpr int PF = 4;
         bf16x8_t af[NG];
 #pragma unroll
@@ -1162,17 +1150,13 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
             if (k + PF < NG) af[k + PF] = row_frag(cur, (k + PF) / KS, (k + PF) % KS);
             const int mb = k / KS, ks = k % KS;
             sacc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], wf[ks], sacc[mb], 0, 0, 0);
-            if ((k & 3) == 1 && (k >> 2) < NI) {
-                if (STAGE)
-                    stg[k >> 2] = load_piece(t + 1, k >> 2, pa, pb);
-                else
-                    issue_piece(t + 1, nxt, k >> 2, pa, pb);
-            }
-            if (k >= 2 && k < 8) {
-                const int n = k - 2, b2 = n & 1;
-                if (n < 2) snl[b2] = *reinterpret_cast<const f32x4_t*>(scb + 4 * (16 * b2 + 4 * g));
-                else if (n < 4) sgg[b2] = *reinterpret_cast<const f32x4_t*>(scb + 256 + 4 * (16 * b2 + 4 * g));
-                else syy[b2] = *reinterpret_cast<const int4*>(scb + 512 + 4 * (16 * b2 + 4 * g));
+            if ((k & 3) == 1 && (k >> 2) < NI) issue_piece(t + 1, nxt, k >> 2, pa, pb);
+            if (k >= 2 && k < 10) {  // token 16·b2 + 4g + r's record
+                const int n = k - 2, b2 = n >> 2, r = n & 3;
+                const f32x4_t rec = *reinterpret_cast<const f32x4_t*>(scb + 16 * (16 * b2 + 4 * g + r));
+                snl[b2][r] = rec.x;
+                sgg[b2][r] = rec.y;
+                syy[b2][r] = __float_as_int(rec.z);
             }
             if (k >= KS + 4 && k < KS + 8) dsv(0, k - KS - 4);  // block 0's S is final (+latency)
             __builtin_amdgcn_sched_barrier(0);
@@ -1194,11 +1178,7 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
             if (nb + PFO < DB) tf[nb + PFO] = tr_frag(cur, nb + PFO);
             D[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tf[nb], D[nb], 0, 0, 0);
             const int gk = NG + nb;  // global gap index
-            if (!STAGE && (gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 1, nxt, gk >> 2, pa, pb);
-            if (STAGE && (nb & 3) == 1 && (nb >> 2) < NI) {
-                const int i = wave + G::kWaves * (nb >> 2);
-                *reinterpret_cast<vec4u*>(nxt + i * 1024 + 16 * lane) = stg[nb >> 2];
-            }
+            if ((gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 1, nxt, gk >> 2, pa, pb);
             __builtin_amdgcn_sched_barrier(0);
         }
         LL_TS(ts4);
@@ -1210,137 +1190,17 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
 #endif
         (void)ts1, (void)ts2, (void)ts3, (void)ts4;
     };
-    if (!PIPE) {
-        for (int t = t0; t < t1; ++t) {
-            unsigned long long ts0 = 0, ts1 = 0;
-            LL_TS(ts0);
-            __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t
-            ll_lds_barrier();  // every wave's; and every wave is done with tile t-1
-            LL_TS(ts1);
+    for (int t = t0; t < t1; ++t) {
+        unsigned long long ts0 = 0, ts1 = 0;
+        LL_TS(ts0);
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t
+        ll_lds_barrier();  // every wave's; and every wave is done with tile t-1
+        LL_TS(ts1);
 #if LL_STAMP
-            stamp[0] += ts1 - ts0;
+        stamp[0] += ts1 - ts0;
 #endif
-            (void)ts0, (void)ts1;
-            tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, t);
-        }
-    } else if (t0 < t1) {
-        // ---- PIPE: carried between steps — Sᵀ of tile t (sacc) and its token scalars
-        f32x4_t sacc[2] = {f32x4_t{}, f32x4_t{}};
-        f32x4_t snl[2], sgg[2];
-        int4 syy[2];
-        float ds[8];
-        auto dsv = [&](int t, int mb, int r) __attribute__((always_inline)) {
-            const int tb = 16 * mb + 4 * g + r;
-            const float gv = t * kLLRows + tb < nv ? sgg[mb][r] : 0.0f;
-            const float pv = exp2_fast(fmaf(sacc[mb][r], kLog2e, snl[mb][r]));
-            ds[4 * mb + r] = gv * ((syy[mb][r] == vcol ? 1.0f : 0.0f) - pv);
-        };
-        auto read_scalars = [&](const char* slot, int n) __attribute__((always_inline)) {
-            const char* scb = slot + G::kStage;
-            const int b2 = n & 1;
-            if (n < 2) snl[b2] = *reinterpret_cast<const f32x4_t*>(scb + 4 * (16 * b2 + 4 * g));
-            else if (n < 4) sgg[b2] = *reinterpret_cast<const f32x4_t*>(scb + 256 + 4 * (16 * b2 + 4 * g));
-            else syy[b2] = *reinterpret_cast<const int4*>(scb + 512 + 4 * (16 * b2 + 4 * g));
-        };
-        auto dw_phase = [&](const char* __restrict__ cur, char* __restrict__ fut, const bf16x8_t& da,
-                            const vec4u* stg) __attribute__((always_inline)) {
-            constexpr int PFO = 4;
-            bf16x8_t tf[DB];
-#pragma unroll
-            for (int nb = 0; nb < PFO; ++nb) tf[nb] = tr_frag(cur, nb);
-#pragma unroll
-            for (int nb = 0; nb < DB; ++nb) {
-                if (nb + PFO < DB) tf[nb + PFO] = tr_frag(cur, nb + PFO);
-                D[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tf[nb], D[nb], 0, 0, 0);
-                if (STAGE && stg && (nb & 3) == 1 && (nb >> 2) < NI) {
-                    const int i = wave + G::kWaves * (nb >> 2);
-                    *reinterpret_cast<vec4u*>(fut + i * 1024 + 16 * lane) = stg[nb >> 2];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        };
-        char* c0 = smem;
-        char* c1 = smem + kStage;
-        char* c2 = smem + 2 * kStage;
-#pragma unroll
-        for (int k = 0; k < NI; ++k) issue_piece(t0, c0, k, rowA, rowB);
-        if (wave == 0) issue_scalars(t0, c0);
-#pragma unroll
-        for (int k = 0; k < NI; ++k) issue_piece(t0 + 1, c1, k, nrowA, nrowB);
-        if (wave == 0) issue_scalars(t0 + 1, c1);
-        nrowA = tok_row((t0 + 2) * kLLRows + rA);
-        nrowB = tok_row((t0 + 2) * kLLRows + rB);
-        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));
-        ll_lds_barrier();
-#pragma unroll
-        for (int k = 0; k < NG; ++k)
-            sacc[k / KS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag(c0, k / KS, k % KS), wf[k % KS],
-                                                                   sacc[k / KS], 0, 0, 0);
-#pragma unroll
-        for (int n = 0; n < 6; ++n) read_scalars(c0, n);
-        // step t: cur (tile t), nx (tile t+1, landed), fut (tile t+2); the regions as
-        // __restrict__ parameters (alias scopes: no DMA wait before the reads of nx)
-        auto step = [&](const char* __restrict__ cur, const char* __restrict__ nx, char* __restrict__ fut,
-                        int t) __attribute__((always_inline)) {
-            unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
-            LL_TS(ts0);
-            __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t+1
-            ll_lds_barrier();  // every wave's; and every wave is done with tile t-1 (= c2)
-            LL_TS(ts1);
-            const int pa = a.rows ? nrowA : min((t + 2) * kLLRows + rA, nv - 1);  // tile t+2's rows
-            const int pb = a.rows ? nrowB : min((t + 2) * kLLRows + rB, nv - 1);
-            nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rA, nv - 1) * 4, 0, 0);
-            nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rB, nv - 1) * 4, 0, 0);
-            vec4u stg[STAGE ? NI : 1];
-            f32x4_t sn[2] = {f32x4_t{}, f32x4_t{}};
-            bf16x8_t da;
-            // ---- phase 1, gap k: row read k+PF of tile t+1 | MFMA k of Sᵀ(t+1) | piece of
-            // tile t+2 every 4th gap | dS(t) in the even gaps 0..14 | tile t+1's scalars 18..23
-            constexpr int PF = 4;
-            bf16x8_t af[NG];
-#pragma unroll
-            for (int k = 0; k < PF; ++k) af[k] = row_frag(nx, k / KS, k % KS);
-#pragma unroll
-            for (int k = 0; k < NG; ++k) {
-                if (k + PF < NG) af[k + PF] = row_frag(nx, (k + PF) / KS, (k + PF) % KS);
-                sn[k / KS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], wf[k % KS], sn[k / KS], 0, 0, 0);
-                if ((k & 3) == 1 && (k >> 2) < NI) {
-                    if (STAGE)
-                        stg[k >> 2] = load_piece(t + 2, k >> 2, pa, pb);
-                    else
-                        issue_piece(t + 2, fut, k >> 2, pa, pb);
-                }
-                if (k < 16 && (k & 1) == 0) dsv(t, k >> 3, (k >> 1) & 3);
-                if (k == 16) da = pack8(ds);  // A operand: slot 8g + j <- token t(g, j)
-                if (k >= 18 && k < 24) read_scalars(nx, k - 18);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (wave == 0) issue_scalars(t + 2, fut);
-            LL_TS(ts2);
-            dw_phase(cur, fut, da, STAGE ? stg : nullptr);
-            LL_TS(ts3);
-#if LL_STAMP
-            stamp[0] += ts1 - ts0;
-            stamp[1] += ts2 - ts1;
-            stamp[3] += ts3 - ts2;
-            stamp[6] += 1;
-#endif
-            (void)ts0, (void)ts1, (void)ts2, (void)ts3;
-            sacc[0] = sn[0];
-            sacc[1] = sn[1];
-        };
-        for (int t = t0; t + 1 < t1; ++t) {
-            step(c0, c1, c2, t);
-            char* cc = c0;
-            c0 = c1;
-            c1 = c2;
-            c2 = cc;
-        }
-        // the last tile: its dS and dW
-#pragma unroll
-        for (int q = 0; q < 8; ++q) dsv(t1 - 1, q >> 2, q & 3);
-        const bf16x8_t da = pack8(ds);
-        dw_phase(c0, c2, da, nullptr);
+        (void)ts0, (void)ts1;
+        tile(smem + ((t - t0) & 1) * kStage, smem + ((t + 1 - t0) & 1) * kStage, t);
     }
 #if LL_STAMP
     if (lane == 0 && blockIdx.x * 4 + wave < (1 << 12))
@@ -1394,20 +1254,12 @@ static thread_local int g_ll_tsplit = 0;  // tuning "lmloss_dw_tsplit" (0 = auto
 // (ll_fwd16_block: no exchange, but twice the LDS bytes per MFMA — measured 1123 vs ~1010 us
 // at C2, while the same trade won for dW, whose exchange and dS sat on the critical path)
 static thread_local int g_ll_fwd = 0;
-static thread_local int g_ll_dw_stage = 0;  // tuning "lmloss_dw_stage": bit 0 register-staged, bit 1 pipelined
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
     const bool sp = key && !__builtin_strcmp(key, "lmloss_splits");
     const bool ts = key && !__builtin_strcmp(key, "lmloss_dw_tsplit");
     const bool fw = key && !__builtin_strcmp(key, "lmloss_fwd");
-    const bool dst = key && !__builtin_strcmp(key, "lmloss_dw_stage");
-    *handled = sp || ts || fw || dst;
-    if (dst) {
-        TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG,
-                     "lmloss_dw_stage: 0 LDS-DMA, 1 register-staged, 2 pipelined (3 stages), 3 both");
-        g_ll_dw_stage = int(value);
-        return TRLX_OK;
-    }
+    *handled = sp || ts || fw;
     if (fw) {
         TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "lmloss_fwd: 0 auto (1), 1 32x32 pair form, 2 16x16 form");
         g_ll_fwd = int(value);
@@ -1428,9 +1280,7 @@ static size_t ll_align(size_t x) { return (x + 255) & ~size_t(255); }
 struct LlWs {
     float* opart;
     float2* mlpart;
-    float* nlse;
-    float* gbuf;
-    int* ybuf;
+    float* trec;
     int* order;
     int* cnt;
     int* flags;
@@ -1482,9 +1332,7 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w) {
     LlWs t;
     t.opart = reinterpret_cast<float*>(take(size_t(kLLMaxSplits) * N * H * 4));
     t.mlpart = reinterpret_cast<float2*>(take(size_t(kLLMaxSplits) * N * 8));
-    t.nlse = reinterpret_cast<float*>(take(size_t(N) * 4));
-    t.gbuf = reinterpret_cast<float*>(take(size_t(N) * 4));
-    t.ybuf = reinterpret_cast<int*>(take(size_t(N) * 4));
+    t.trec = reinterpret_cast<float*>(take(size_t(N) * 16));
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t(order_chunks(N) + 1) * 4));
     t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 4 * 4));  // <= 4 waves per workgroup
@@ -1526,11 +1374,7 @@ static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
 }
 template <class G>
 static int ll_launch_dw(const LmLossArgs& a, hipStream_t s) {
-    void (*k)(LmLossArgs) = g_ll_dw_stage == 1   ? k_lmloss_dw<G, true, false>
-                            : g_ll_dw_stage == 2 ? k_lmloss_dw<G, false, true>
-                            : g_ll_dw_stage == 3 ? k_lmloss_dw<G, true, true>
-                                                 : k_lmloss_dw<G, false, false>;
-    hipLaunchKernelGGL(k, dim3(unsigned(a.dw_full + a.dw_nblk * a.tsplit)), dim3(G::kThreads), 0, s, a);
+    hipLaunchKernelGGL(k_lmloss_dw<G>, dim3(unsigned(a.dw_full + a.dw_nblk * a.tsplit)), dim3(G::kThreads), 0, s, a);
     return check_launch("k_lmloss_dw");
 }
 static int ll_fwd(const LmLossArgs& a, hipStream_t s) {
@@ -1567,9 +1411,7 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.dwpart = w.dwpart;
     a.opart = w.opart;
     a.mlpart = w.mlpart;
-    a.nlse = w.nlse;
-    a.gbuf = w.gbuf;
-    a.ybuf = w.ybuf;
+    a.trec = w.trec;
     a.flags = w.flags;
     a.dw = dweight;
     a.lddw = lddw;
