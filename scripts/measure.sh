@@ -44,6 +44,7 @@ for st in $steps; do
                  run ${TAG}_sched_rccl_serial_$i 200 $B --steps 200 --warmup 5 --dist --schedule serial
                  run ${TAG}_sched_rccl_pipe_$i 200 $B --steps 200 --warmup 5 --dist --schedule pipelined
                done ;;
+        mfma) run ${TAG}_pmc_mfma_lossside_c2 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/${TAG}_pmc_mfma_c2 -o run -- python3 tools/lossside_bench.py --config c2 --rounds 1 --iters 3 ;;
         smoke) run ${TAG}_smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
         *) echo "unknown step $st"; exit 2 ;;
     esac
