@@ -188,7 +188,7 @@ def store_padded(x, lengths):
     element covers its own decoder length and the collate pads with 0.0 (lengths None: as is)."""
     if lengths is None:
         return x
-    return x.masked_fill(torch.arange(x.shape[1])[None, :] >= lengths[:, None], 0)
+    return x.masked_fill(torch.arange(x.shape[1], device=x.device)[None, :] >= lengths[:, None], 0)
 
 
 def kl_penalty_rewards(logprobs, ref_logprobs, kl_coef, scores=None, lengths=None):
@@ -201,10 +201,10 @@ def kl_penalty_rewards(logprobs, ref_logprobs, kl_coef, scores=None, lengths=Non
             rewards[:, -1] += scores
         return rewards
     T = rewards.shape[1]
-    pad = torch.arange(T)[None, :] >= lengths[:, None]
+    pad = torch.arange(T, device=rewards.device)[None, :] >= lengths[:, None]
     rewards = rewards.masked_fill(pad, 0)
     if scores is not None:
-        rows = torch.arange(rewards.shape[0])
+        rows = torch.arange(rewards.shape[0], device=rewards.device)
         rewards[rows, lengths - 1] += scores
     return rewards
 
@@ -231,7 +231,7 @@ def ppo_step_reference(logits, ref_logits, new_logits, labels, old_values, value
             lp, ref_lp, ov = store_padded(lp, lengths), store_padded(ref_lp, lengths), store_padded(ov, lengths)
         rewards = kl_penalty_rewards(lp, ref_lp, kl_coef, scores, lengths)
     if mask is None:
-        mask = torch.ones((B, T), dtype=torch.long)
+        mask = torch.ones((B, T), dtype=torch.long, device=labels.device)
     adv, ret = gae(ov, rewards, T, cfg["gamma"], cfg["lam"], use_whitening=True)
     x = new_logits.detach().clone().requires_grad_(True)
     v = values.detach().clone().requires_grad_(True)

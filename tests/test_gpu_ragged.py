@@ -185,6 +185,53 @@ def test_ragged_step_vs_oracle(B, Tn, V, dt):
             assert st[i] == pytest.approx(float(ref["stats"][k]), rel=1e-5, abs=1e-6), (split, k)
 
 
+
+@pytest.mark.parametrize("B,Tn,V,ragged", [(256, 48, 32128, True), (128, 48, 50257, False)])
+def test_bench_shard_vs_oracle(B, Tn, V, ragged):
+    """The bench's shards at full size — C3: 256 rollouts x 48 decoder tokens x V 32128 with
+    ragged decoder lengths, the padded rows NaN; C2: 128 x 48 x V 50257 dense — bf16 logits
+    through PPOHotPath.step, against the oracle's reference ops run on the GPU in fp32 on the
+    clean batch (the C3 path was pinned only at B <= 16)."""
+    g = torch.Generator(device=DEV).manual_seed(512)
+    f = dict(generator=g, device=DEV)
+    logits = torch.randn(B, Tn, V, **f).to(torch.bfloat16)
+    ref_logits = (logits.float() + 0.1 * torch.randn(B, Tn, V, **f)).to(torch.bfloat16)
+    new_logits = (logits.float() + 0.05 * torch.randn(B, Tn, V, **f)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, Tn), **f)
+    old_values = torch.randn(B, Tn, **f)
+    values = old_values + 0.3 * torch.randn(B, Tn, **f)
+    scores = torch.rand(B, **f) * 24 - 12
+    L = torch.randint(1, Tn + 1, (B,), **f) if ragged else torch.full((B,), Tn, device=DEV)
+    L[0] = Tn
+    pad = torch.arange(Tn, device=DEV)[None, :] >= L[:, None]
+    mask = (~pad).long()
+    old_values = old_values.masked_fill(pad, 0)
+    if not ragged:
+        L = mask = None
+    ref = orc.ppo_step_reference(logits.float(), ref_logits.float(), new_logits.float(), labels, old_values, values,
+                                 scores, kl_coef=0.05, lengths=L, mask=mask)
+    lg, rl, nl = logits.clone(), ref_logits.clone(), new_logits.clone()
+    lg[pad] = float("nan")
+    rl[pad] = float("nan")
+    nl[pad] = float("nan")
+    hp = P.PPOHotPath(P.PPOConfig(), B, Tn, V, torch.bfloat16, DEV, kl_coef=0.05)
+    loss, stats, dl, dv = hp.step(lg, rl, nl, labels, old_values, values, scores, lengths=L, mask=mask)
+    hp.wait_stats()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(hp.lp_old, ref["lp"], **RT32)
+    torch.testing.assert_close(hp.ref_lp, ref["ref_lp"], **RT32)
+    torch.testing.assert_close(hp.rewards, ref["rewards"], **RT32)
+    torch.testing.assert_close(hp.returns, ref["returns"], rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(hp.lp_new, loss_rows_lp(ref["new_lp"], mask), **RT32)
+    torch.testing.assert_close(loss.reshape(()), ref["loss"].detach().reshape(()), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dv, ref["dvalues"], rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(dl.float(), ref["dlogits"], rtol=8e-3, atol=1e-9)
+    assert torch.equal(dl[pad].float().abs().sum(), torch.zeros((), device=DEV))
+    st = stats.cpu().tolist()
+    for i, k in enumerate(P.STATS_KEYS):
+        assert st[i] == pytest.approx(float(torch.as_tensor(ref["stats"][k]).detach()), rel=1e-5, abs=1e-6), k
+
+
 def test_ragged_pipeline_matches_step():
     """The pipelined schedule (ragged experience rows inside the loss-tail launch, masked loss
     rows beside the folded GAE) over three poisoned ragged batches: bit-identical to
