@@ -161,14 +161,30 @@ __device__ __forceinline__ int ll_piece_row(int i, int lane) { return 8 * ((i & 
 // kernel's and does not put a vmcnt(0) in front of the next LDS read (the flat
 // global_load_lds form made every tile wait for the DMA of the NEXT one before its first read).
 // The byte offset in the row-major source of the 16 B that lane `lane` of piece i carries.
-__device__ __forceinline__ int ll_piece_src(int i, int row_bytes, int lane) {
+// The 16x16x32 forms' image (S16) swizzles the 16-B slot with ll16_swz((r>>2)&3) instead of
+// (r>>2)&3: their row reads (16 rows x 4 chunks) and transposed reads (rows r, r+4 of a
+// subtile in one 32-lane group) were 2-way bank-conflicted on the 32x32 image (PMC:
+// SQ_LDS_BANK_CONFLICT = 48 % of the dW kernel's LDS cycles), conflict-free on this one.
+__device__ __forceinline__ int ll16_swz(int R) { return (0x78 >> (2 * R)) & 3; }  // 0 2 3 1
+__device__ __forceinline__ int ll_piece_src_sw(int i, int row_bytes, int lane, bool s16) {
     const int r = ll_piece_row(i, lane);
-    const int ch = 4 * (2 * (i & 1) + (lane >> 5)) + ((lane & 3) ^ ((r >> 2) & 3));
+    const int sw = s16 ? ll16_swz((r >> 2) & 3) : ((r >> 2) & 3);
+    const int ch = 4 * (2 * (i & 1) + (lane >> 5)) + ((lane & 3) ^ sw);
     return row_bytes + (i >> 3) * 256 + ch * 16;
+}
+__device__ __forceinline__ int ll_piece_src(int i, int row_bytes, int lane) {
+    return ll_piece_src_sw(i, row_bytes, lane, false);
+}
+__device__ __forceinline__ int ll16_piece_src(int i, int row_bytes, int lane) {
+    return ll_piece_src_sw(i, row_bytes, lane, true);
 }
 __device__ __forceinline__ void ll_piece(char* slot, int i, __amdgpu_buffer_rsrc_t rs, int row_bytes, int lane) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
                                              ll_piece_src(i, row_bytes, lane), 0, 0, 0);
+}
+__device__ __forceinline__ void ll16_piece(char* slot, int i, __amdgpu_buffer_rsrc_t rs, int row_bytes, int lane) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
+                                             ll16_piece_src(i, row_bytes, lane), 0, 0, 0);
 }
 
 // Per-lane byte offsets of the two operand reads inside a staged tile, for a wave whose hidden
@@ -363,11 +379,11 @@ typedef LlGeom<512, 2, 2> LlG512;
 //     ll16_trb[nb&1] + (nb>>3)·8192 + ((nb&7)>>1)·512 (+4096)
 __device__ __forceinline__ int ll16_rb(int lane) {
     const int g = lane >> 4, c = lane & 15;
-    return 2048 * (c >> 3) + 64 * (c & 7) + 16 * (g ^ ((c >> 2) & 3));
+    return 2048 * (c >> 3) + 64 * (c & 7) + 16 * (g ^ ll16_swz((c >> 2) & 3));
 }
 __device__ __forceinline__ int ll16_trb(int lane, int par) {
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    return 2048 * (g >> 1) + 64 * (4 * (g & 1) + q) + 16 * ((2 * par + (p >> 1)) ^ g) + 8 * (p & 1);
+    return 2048 * (g >> 1) + 64 * (4 * (g & 1) + q) + 16 * ((2 * par + (p >> 1)) ^ ll16_swz(g)) + 8 * (p & 1);
 }
 __device__ __forceinline__ bf16x8_t ll16_row_frag(const char* tile, int rb, int mb, int ks) {
     return *reinterpret_cast<const bf16x8_t*>(tile + rb + 4096 * mb + (ks >> 2) * 8192 + (ks & 3) * 512);
@@ -707,7 +723,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
         const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
-        ll_piece(slot, i, rw, t < t1 ? off : int(0x7ffff000), lane);
+        ll16_piece(slot, i, rw, t < t1 ? off : int(0x7ffff000), lane);
     };
     const int rb = ll16_rb(lane);
     const int trb[2] = {ll16_trb(lane, 0), ll16_trb(lane, 1)};
@@ -1092,7 +1108,7 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
         // 24-bit multiply (rows < 2^24, row bytes < 2^24): a 32-bit product here became a
         // v_mad_u64_u32 whose unused high addend register was a pending load's destination
         const int rbytes = int(__umul24(uint32_t(((i & 7) == (wave & 7)) ? ra : rbw), uint32_t(a.ldh) * 2u));
-        const int off = ll_piece_src(i, rbytes, lane);
+        const int off = ll16_piece_src(i, rbytes, lane);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
                                                  t < t1 ? off : int(0x7ffff000), 0, 0, 0);
     };
