@@ -61,6 +61,11 @@ def parse():
     p.add_argument("--no-fp32-line", action="store_true",
                    help="PPO C2 at N=1: skip the secondary fp32-logits measurement (reported under fp32_logits)")
     p.add_argument("--no-timers", action="store_true", help="skip per-kernel HIP events")
+    p.add_argument("--no-from-hidden", action="store_true",
+                   help="PPO C2 at N=1: skip the secondary §8f-2 loss-side measurement (reported under from_hidden: "
+                        "the PPO update from hidden states, fused MFMA route vs the hipBLASLt logits route)")
+    p.add_argument("--from-hidden-steps", type=int, default=10,
+                   help="updates per route and round of the from_hidden measurement (3 interleaved rounds)")
     p.add_argument("--host-state", action="store_true",
                    help="PPO: keep beta as a host constant and skip the score RunningMoments/clip and the KL "
                         "controller update (the default runs them on device, ppo_config.yml settings)")
@@ -398,6 +403,79 @@ def cpu_baseline(torch, T, V, seconds, dtype=None):
                       f"AdaptiveKLController: reference ops incl. autograd backward), {el:.1f} s, torch.set_num_threads({cores})"}
 
 
+MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16: 1024 FLOP/clk/SIMD x 4 SIMD x 256 CU x 2.4 GHz (MI355X_MICROARCH.md)
+FROM_HIDDEN_SHAPES = {  # name: (rows, T, V, H, masked) — BASELINE configs[1] and a configs[2] DP2 shard
+    "c2": (128, 48, 50257, 768, False),
+    "c3_shard": (256, 48, 32128, 768, True),
+}
+
+
+def from_hidden_leg(torch, P, dev, name, steps, rounds=3):
+    """§8f-2, loss side, as the driver runs it: the PPO update from the policy's hidden states
+    (PPOHotPath.policy_loss_from_hidden after one experience_from_hidden), the fused MFMA route
+    (csrc/lmhead_loss.hip: no [N, V] logits / dlogits in HBM) against the reference's structure on
+    the hot path's kernels (route "gemm": hipBLASLt bf16 logits -> fused loss rows -> hipBLASLt
+    dh and dW GEMMs), `steps` updates per route per round, rounds interleaved (the first route
+    alternates), HIP events on the launch stream around each round; the deferred loss tail of
+    every update runs inside the timed region.  Per-update times are the median over rounds."""
+    B, T, V, H, masked = FROM_HIDDEN_SHAPES[name]
+    g = torch.Generator(device=dev).manual_seed(4242)
+    f = dict(generator=g, device=dev)
+    h = torch.randn(B, T, H, **f).to(torch.bfloat16)
+    w = (0.05 * torch.randn(V, H, **f)).to(torch.bfloat16)
+    ref_h = (h.float() + 0.1 * torch.randn(B, T, H, **f)).to(torch.bfloat16)
+    new_h = (h.float() + 0.05 * torch.randn(B, T, H, **f)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (B, T), **f)
+    old_values = torch.randn(B, T, **f)
+    values = old_values + 0.3 * torch.randn(B, T, **f)
+    scores = torch.rand(B, **f) * 24 - 12
+    lengths = mask = None
+    if masked:
+        lengths = torch.randint(1, T + 1, (B,), **f)
+        mask = (torch.arange(T, device=dev)[None, :] < lengths[:, None]).long()
+    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05, defer_tail=True)
+    hp.experience_from_hidden(h, w, ref_h, w, labels, old_values, scores, lengths=lengths, mask=mask, route="fused")
+
+    def upd(route):
+        hp.policy_loss_from_hidden(new_h, w, labels, values, old_values, mask=mask, route=route)
+
+    for route in ("fused", "gemm", "fused"):  # ~50 ms of load first: an idle chip runs slow (settle_and_warm)
+        for _ in range(8):
+            upd(route)
+    hp.wait_stats()
+    torch.cuda.synchronize()
+    times = {"fused": [], "gemm": []}
+    for r in range(rounds):
+        for route in (("fused", "gemm") if r % 2 == 0 else ("gemm", "fused")):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps):
+                upd(route)
+            hp.wait_stats()
+            e1.record()
+            torch.cuda.synchronize()
+            times[route].append(e0.elapsed_time(e1) / steps)
+    nv = int(mask.sum().item()) if masked else B * T
+    fused_ms = sorted(times["fused"])[len(times["fused"]) // 2]
+    gemm_ms = sorted(times["gemm"])[len(times["gemm"]) // 2]
+    flop = 4 * 2 * nv * V * H  # the fused route's four MFMA passes over the live tokens
+    ach = flop / (fused_ms * 1e-3) / 1e12
+    out = {"shape": {"rows": B, "seq_len": T, "vocab": V, "hidden": H, "tokens": B * T, "live_tokens": nv,
+                     "masked": masked},
+           "fused_ms_per_update": round(fused_ms, 4), "gemm_ms_per_update": round(gemm_ms, 4),
+           "fused_vs_gemm": round(gemm_ms / fused_ms, 4),
+           "rounds_ms": {k: [round(v, 4) for v in vs] for k, vs in times.items()},
+           "roofline": {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "flop_per_update": flop,
+                        "note": "4 N·V·H multiply-add passes (S, O = P·W forward; S recomputed, dSᵀ·h backward) over "
+                                "the live tokens, per fused update (combine, compaction and loss tail included in "
+                                "the time)"},
+           "steps_per_round": steps, "rounds": rounds}
+    del hp, h, w, ref_h, new_h
+    torch.cuda.empty_cache()
+    return out
+
+
 SETTLE_CHUNK = 8  # steps between the ranks' agreement on whether the settle is over (N > 1)
 
 
@@ -624,6 +702,14 @@ def main():
         del hp32, step32, x32
         torch.cuda.empty_cache()
 
+    # Secondary line (C2 at N=1): §8f-2's loss side from hidden states (the fused
+    # route's speed-up over the hipBLASLt logits route, measured by the driver's run)
+    from_hidden = None
+    if (not ilql and world == 1 and args.config == "c2" and args.logits_dtype == "bf16" and not args.no_from_hidden
+            and not args.global_batch):
+        from_hidden = {name: from_hidden_leg(torch, P, dev, name, args.from_hidden_steps)
+                       for name in FROM_HIDDEN_SHAPES}
+
     out = None
     if rank == 0:
         cpu = None
@@ -669,6 +755,8 @@ def main():
         }
         if fp32_line:
             out["fp32_logits"] = fp32_line
+        if from_hidden:
+            out["from_hidden"] = from_hidden
         print(json.dumps(out), flush=True)
     if use_dist:
         dist.barrier()

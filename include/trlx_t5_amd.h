@@ -358,12 +358,15 @@ int trlx_lmhead_logprobs_ragged(const void* hidden, int64_t ldh, const void* wei
  * accumulates dSᵀ·h; deterministic (fixed-order sums, no atomics).
  * lm_workspace: trlx_lmhead_loss_workspace_bytes(N, H, V) bytes, no initialisation. */
 int64_t trlx_lmhead_loss_workspace_bytes(int64_t N, int64_t H, int64_t V);
+/* The smaller workspace trlx_lmhead_logprobs_bwd needs (no forward partials). */
+int64_t trlx_lmhead_loss_bwd_workspace_bytes(int64_t N, int64_t H, int64_t V);
 /* The PPO loss from the policy's last hidden states: trlx_ppo_loss_rows's arguments with the
  * logits replaced by (hidden, weight) and dlogits by (dhidden, dweight) — same token records
  * in `workspace` (trlx_ppo_rollout_loss then emits loss + stats), same whitening of adv_raw by
- * `stats` (NULL: adv_raw used as given), dvalues, lp_out.  Tokens with mask == 0 are skipped
- * (compacted out of all three MFMA passes: zero gradient, lp_out 0, their token records as
- * the masked loss rows write them). */
+ * `stats` (NULL: adv_raw used as given, and then only mask = NULL: the loss normaliser Σ mask
+ * is read at stats[3]), dvalues, lp_out.  Tokens with mask == 0 are skipped (compacted out of
+ * all three MFMA passes: zero gradient, lp_out 0, their token records as the masked loss rows
+ * write them).  N·ldh·2 and V·ldw·2 must stay below 2 GB (32-bit tile addressing). */
 int trlx_ppo_loss_from_hidden(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B,
                               int64_t T, int64_t H, int64_t V, const int64_t* labels, const void* old_lp,
                               int old_dtype, const float* adv_raw, const double* stats, int unbiased,
@@ -372,9 +375,27 @@ int trlx_ppo_loss_from_hidden(const void* hidden, int64_t ldh, const void* weigh
                               float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
                               int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues,
                               void* workspace, void* lm_workspace, void* stream);
+/* The split-beta form (the pipelined data-parallel schedule; see trlx_ppo_loss_rows_split /
+ * trlx_ppo_loss_rows_split_gae): the advantage A0 - beta*Ak whitened by coefficients that are
+ * either given (`coef`, stored by an earlier loss on the same experience) or derived here from
+ * the all-reduced split record `stats8` and beta (ctl_state[TRLX_CTL_KL_COEF], or kl_coef when
+ * ctl_state is NULL; `unbiased` as there) and stored to coef_out (may be NULL) — exactly one of
+ * coef / stats8.  The batch's rewards and returns (r_dtype) are written here; msum = Σ mask
+ * (stats8 + 6; required with a mask); the loss tail takes stats8 + 3 as its `stats`. */
+int trlx_ppo_loss_from_hidden_split(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B,
+                                    int64_t T, int64_t H, int64_t V, const int64_t* labels, const void* old_lp,
+                                    int old_dtype, const float* adv0, const float* adv_kl, const float* rew_kl,
+                                    const float* rew_score, const float* coef, const double* stats8, int unbiased,
+                                    const double* ctl_state, float kl_coef, float* coef_out, const double* msum,
+                                    const int64_t* mask, const void* values, int v_dtype, const void* old_values,
+                                    int ov_dtype, float* rewards, void* returns, int r_dtype, float cliprange,
+                                    float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
+                                    int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues,
+                                    void* workspace, void* lm_workspace, void* stream);
 /* The differentiable building block (logprobs_from_logits(lm_head(h), y) with autograd):
  * forward -> lp [N] (lp_dtype), lse [N] fp32 and E = Σ_v p_tv·W_v [N, H] fp32 (saved for the
- * backward); backward(grad = d loss / d lp [N], F32 / BF16) -> dhidden, dweight. */
+ * backward); backward(grad = d loss / d lp [N], F32 / BF16) -> dhidden, dweight (either may be
+ * NULL: a frozen lm_head skips the dW pass; lm_workspace: trlx_lmhead_loss_bwd_workspace_bytes). */
 int trlx_lmhead_logprobs_fwd_saved(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                                    int64_t H, int64_t V, const int64_t* labels, int64_t lb, void* lp_out,
                                    int lp_dtype, float* lse_out, float* e_out, void* lm_workspace, void* stream);

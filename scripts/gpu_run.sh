@@ -57,6 +57,9 @@ for step in "$@"; do
                      -o run -- python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-timers ;;
         pmc_write) run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write \
                      -o run -- python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-timers ;;
+        newtests) run new_tests 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread -p no:cacheprovider \
+                     tests/test_gpu_lmhead_loss.py tests/test_gpu_dist_hidden.py tests/test_gpu_dist_world.py ;;
+        bench20) run bench20 400 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -270,3 +270,53 @@ def rccl_scores_reuse_worker(port, inputs, q):
     q.put(res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def pipeline_hidden_worker(rank, world, port, batches, q, loss_norm="rank", use_ctl=False):
+    """§8f-2 under the data-parallel schedule: the same batches through step_from_hidden (serial,
+    split beta) and pipeline_step_from_hidden (the lm_head experience of batch k+1 ahead of the
+    loss side of batch k, the whitening all-reduce of batch k in flight meanwhile) on this
+    rank's contiguous row shards (accelerate_ppo_model.py:146-148).  Returns every batch's
+    outputs of both schedules (numpy, pickled by value)."""
+    import torch.distributed as dist
+    import trlx_t5_amd as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    shards = [{k: (v.chunk(world, dim=0)[rank].contiguous().to(dev) if v is not None and k != "w" else
+                   (v.to(dev) if v is not None else None)) for k, v in b.items()} for b in batches]
+    B, T, _ = shards[0]["h"].shape
+    V = shards[0]["w"].shape[0]
+    res = {}
+    for mode in ("serial", "pipelined"):
+        cfg = P.PPOConfig()
+        ctl = P.PPOControlState.from_config(cfg, dev, n_steps=B) if use_ctl else None
+        hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, ctl=ctl, defer_tail=True, split_beta=True,
+                          loss_norm=loss_norm)
+        outs = []
+
+        def grab(o):
+            loss, stats, dh, dw, dv = o
+            hp.wait_stats()
+            torch.cuda.synchronize()
+            outs.append([loss.cpu().numpy(), stats.cpu().numpy(), dh.float().cpu().numpy(), dw.float().cpu().numpy(),
+                         dv.cpu().numpy(), hp.rewards.cpu().numpy(), hp.returns.cpu().numpy()])
+
+        for sh in shards:
+            args = (sh["h"], sh["w"], sh["ref_h"], sh["w"], sh["new_h"], sh["labels"], sh["old_values"], sh["values"],
+                    sh["scores"])
+            kw = dict(lengths=sh["lengths"], mask=sh["mask"], route="fused", loss_route="fused")
+            if mode == "serial":
+                grab(hp.step_from_hidden(*args, **kw))
+            else:
+                o = hp.pipeline_step_from_hidden(*args, **kw)
+                if o is not None:
+                    grab(o)
+        if mode == "pipelined":
+            grab(hp.pipeline_flush())
+        hp.wait_stats()
+        torch.cuda.synchronize()
+        res[mode] = (outs, ctl.state.cpu().numpy() if use_ctl else None)
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -9,6 +9,18 @@
 
 namespace trlx {
 
+// A launch-geometry knob (trlx_set_tuning): one process-wide value, read by whichever host
+// thread launches (PyTorch runs backward nodes on its autograd device thread, so a
+// thread-local knob set by the caller would not reach them).
+struct TuneKnob {
+    int v;
+    operator int() const { return __atomic_load_n(&v, __ATOMIC_RELAXED); }
+    TuneKnob& operator=(int x) {
+        __atomic_store_n(&v, x, __ATOMIC_RELAXED);
+        return *this;
+    }
+};
+
 constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kMaxThreads = 1024;  // largest workgroup we launch
 constexpr float kLog2e = 1.4426950408889634f;

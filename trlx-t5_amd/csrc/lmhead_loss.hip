@@ -48,6 +48,8 @@ constexpr int kLLRows = 32;            // rows of a staged tile: vocab rows (for
 constexpr int kLLMaxSplits = 8;        // vocab splits of the forward (workspace sizing)
 constexpr int kLLTokBlock = 64;        // tokens per forward workgroup (LlGeom: NG = 2 groups of 32)
 constexpr float kLLOverflow = 60.0f;
+// byte span bound of the hidden / weight buffer resources (below the 0x7ffff000 sentinel)
+constexpr int64_t kLLMaxSpan = 0x7fff0000;
 // Diagnostic builds only (-DLL_ABLATE=bits, never the shipped library): drop parts of the
 // forward's steady-state step to price them — 1 softmax, 2 group-sum exchange, 4 next DMA,
 // 8 O product, 16 S product.  Results are wrong in such a build.
@@ -1017,6 +1019,7 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
         reinterpret_cast<f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4] = e;
         return;
     }
+    if (MODE == kLLBwd && !a.dh) return;  // hidden needs no gradient: the dW kernel's record only
     f32x4_t d;
     d.x = g * (bf_lo(wv.x) - e.x);
     d.y = g * (bf_hi(wv.x) - e.y);
@@ -1264,12 +1267,12 @@ __global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int
 }
 
 // ------------------------------------------------------------------ host side
-static thread_local int g_ll_splits = 0;  // tuning "lmloss_splits" (0 = auto)
-static thread_local int g_ll_tsplit = 0;  // tuning "lmloss_dw_tsplit" (0 = auto)
+static TuneKnob g_ll_splits{0};  // tuning "lmloss_splits" (0 = auto)
+static TuneKnob g_ll_tsplit{0};  // tuning "lmloss_dw_tsplit" (0 = auto)
 // tuning "lmloss_fwd": 0 auto (= 1), 1 the 32x32x16 pair form (ll_fwd_block), 2 the 16x16x32 form
 // (ll_fwd16_block: no exchange, but twice the LDS bytes per MFMA — measured 1123 vs ~1010 us
 // at C2, while the same trade won for dW, whose exchange and dS sat on the critical path)
-static thread_local int g_ll_fwd = 0;
+static TuneKnob g_ll_fwd{0};
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
     const bool sp = key && !__builtin_strcmp(key, "lmloss_splits");
@@ -1337,7 +1340,8 @@ static LlDwPlan ll_dw_plan(int64_t V) {
 }
 
 // Workspace carve-up for N tokens (dwpart: the split blocks' fp32 partials).
-static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w) {
+// fwd = false: the backward's carve-up (trlx_lmhead_logprobs_bwd), no forward partials.
+static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, bool fwd = true) {
     char* p = static_cast<char*>(base);
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -1346,8 +1350,8 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w) {
         return q;
     };
     LlWs t;
-    t.opart = reinterpret_cast<float*>(take(size_t(kLLMaxSplits) * N * H * 4));
-    t.mlpart = reinterpret_cast<float2*>(take(size_t(kLLMaxSplits) * N * 8));
+    t.opart = reinterpret_cast<float*>(take(fwd ? size_t(kLLMaxSplits) * N * H * 4 : 0));
+    t.mlpart = reinterpret_cast<float2*>(take(fwd ? size_t(kLLMaxSplits) * N * 8 : 0));
     t.trec = reinterpret_cast<float*>(take(size_t(N) * 16));
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t(order_chunks(N) + 1) * 4));
@@ -1370,6 +1374,11 @@ static int ll_check(const void* hidden, int64_t ldh, const void* weight, int64_t
                  "row strides must be >= H and multiples of 8 elements (16-B rows)");
     TRLX_REQUIRE((reinterpret_cast<uintptr_t>(hidden) & 15) == 0 && (reinterpret_cast<uintptr_t>(weight) & 15) == 0,
                  TRLX_ERR_STRIDE, "hidden / weight must be 16-B aligned");
+    // the tile DMAs address hidden / weight rows through 32-bit buffer resources with int byte
+    // offsets (and an out-of-range sentinel at 0x7ffff000): both spans must stay below it
+    TRLX_REQUIRE(N * ldh * 2 < kLLMaxSpan && V * ldw * 2 < kLLMaxSpan, TRLX_ERR_SHAPE,
+                 "fused lm_head loss: hidden (%lld x %lld) or weight (%lld x %lld) rows span >= 2 GB "
+                 "(split the tokens into chunks)", (long long)N, (long long)ldh, (long long)V, (long long)ldw);
     return TRLX_OK;
 }
 
@@ -1403,7 +1412,8 @@ static int ll_dw(const LmLossArgs& a, hipStream_t s) {
 // the common part: shapes, workspace, optional compaction from the mask
 static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                     int64_t H, int64_t V, const int64_t* labels, int64_t lb, const int64_t* compact_mask,
-                    void* lm_ws, void* dweight, int dw_dtype, int64_t lddw, LlWs& w, hipStream_t s) {
+                    void* lm_ws, void* dweight, int dw_dtype, int64_t lddw, LlWs& w, hipStream_t s,
+                    bool fwd = true) {
     int rc = ll_check(hidden, ldh, weight, ldw, N, H, V);
     if (rc) return rc;
     TRLX_REQUIRE(labels && lm_ws, TRLX_ERR_ARG, "NULL labels / workspace");
@@ -1423,7 +1433,7 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.dw_full = dp.full;
     a.tsplit = dp.tsplit;
     a.dw_nblk = dp.nblk;
-    ll_carve(lm_ws, N, H, V, &w);
+    ll_carve(lm_ws, N, H, V, &w, fwd);
     a.dwpart = w.dwpart;
     a.opart = w.opart;
     a.mlpart = w.mlpart;
@@ -1458,36 +1468,39 @@ extern "C" int64_t trlx_lmhead_loss_workspace_bytes(int64_t N, int64_t H, int64_
     return int64_t(ll_carve(nullptr, N, H, V, nullptr));
 }
 
-extern "C" int trlx_ppo_loss_from_hidden(
-    const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B, int64_t T, int64_t H, int64_t V,
-    const int64_t* labels, const void* old_lp, int old_dtype, const float* adv_raw, const double* stats, int unbiased,
-    const int64_t* mask, const void* values, int v_dtype, const void* old_values, int ov_dtype, const void* returns,
-    int r_dtype, float cliprange, float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
-    int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues, void* workspace, void* lm_workspace,
-    void* stream) {
-    const hipStream_t s = (hipStream_t)stream;
-    LmLossArgs a = {};
+extern "C" int64_t trlx_lmhead_loss_bwd_workspace_bytes(int64_t N, int64_t H, int64_t V) {
+    return int64_t(ll_carve(nullptr, N, H, V, nullptr, false));
+}
+
+// The PPO loss side from hidden states, once `a` holds the per-token PPO fields (whitening by
+// the unsplit record or the split-beta coefficients): shapes, compaction, the three MFMA
+// launches and the combine.
+static int ll_ppo_loss(LmLossArgs& a, const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B,
+                       int64_t T, int64_t H, int64_t V, const int64_t* labels, const int64_t* mask,
+                       const void* values, int v_dtype, const void* old_values, int ov_dtype, const void* returns,
+                       int r_dtype, float cliprange, float cliprange_value, float vf_coef, float* lp_out,
+                       void* dhidden, int64_t lddh, int dh_dtype, void* dweight, int dw_dtype, int64_t lddw,
+                       float* dvalues, void* workspace, void* lm_workspace, hipStream_t s) {
     LlWs w;
     const int64_t N = B * T;
     TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
-    TRLX_REQUIRE(old_lp && adv_raw && values && old_values && returns && lp_out && dhidden && dweight && dvalues &&
-                 workspace, TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_from_hidden");
+    TRLX_REQUIRE(a.old_lp && values && old_values && returns && lp_out && dhidden && dweight && dvalues && workspace,
+                 TRLX_ERR_ARG, "NULL argument to trlx_ppo_loss_from_hidden");
     TRLX_REQUIRE(dh_dtype == TRLX_BF16 || dh_dtype == TRLX_F32, TRLX_ERR_DTYPE, "dhidden dtype");
     TRLX_REQUIRE(dw_dtype == TRLX_BF16 || dw_dtype == TRLX_F32, TRLX_ERR_DTYPE, "dweight dtype");
+    TRLX_REQUIRE(r_dtype == TRLX_F32 || r_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "returns dtype %d", r_dtype);
     TRLX_REQUIRE(lddh % 4 == 0 && lddh >= H && lddw >= H, TRLX_ERR_STRIDE, "gradient row strides");
+    // the PPO normaliser is Σ mask (ppo_models.py:162,177), read from the record: without it
+    // only the all-ones mask (N) is known here
+    TRLX_REQUIRE(a.msum || !mask, TRLX_ERR_ARG,
+                 "trlx_ppo_loss_from_hidden: a mask needs the GAE record (its Σ mask normalises the loss)");
     int rc = ll_setup(a, hidden, ldh, weight, ldw, N, H, V, labels, 1, mask, lm_workspace, dweight, dw_dtype, lddw, w,
                       s);
     if (rc) return rc;
     Workspace ws;
     carve_ppo_workspace(workspace, B, T, &ws);
     a.mode = kLLPpo;
-    a.old_lp = old_lp;
-    a.old_dtype = old_dtype;
-    a.adv = adv_raw;
-    a.stats = stats;
-    a.unbiased = unbiased;
     a.mask = mask;
-    a.msum = stats ? stats + 3 : nullptr;
     a.msum_host = double(N);
     a.cliprange = cliprange;
     a.lp_out = lp_out;
@@ -1510,6 +1523,59 @@ extern "C" int trlx_ppo_loss_from_hidden(
     rc = check_launch("k_lmloss_combine");
     if (rc) return rc;
     return ll_dw_finish(a, dweight, dw_dtype, lddw, w, s);
+}
+
+extern "C" int trlx_ppo_loss_from_hidden(
+    const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B, int64_t T, int64_t H, int64_t V,
+    const int64_t* labels, const void* old_lp, int old_dtype, const float* adv_raw, const double* stats, int unbiased,
+    const int64_t* mask, const void* values, int v_dtype, const void* old_values, int ov_dtype, const void* returns,
+    int r_dtype, float cliprange, float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
+    int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues, void* workspace, void* lm_workspace,
+    void* stream) {
+    LmLossArgs a = {};
+    TRLX_REQUIRE(adv_raw, TRLX_ERR_ARG, "NULL adv_raw");
+    a.old_lp = old_lp;
+    a.old_dtype = old_dtype;
+    a.adv = adv_raw;
+    a.stats = stats;
+    a.unbiased = unbiased;
+    a.msum = stats ? stats + 3 : nullptr;
+    return ll_ppo_loss(a, hidden, ldh, weight, ldw, B, T, H, V, labels, mask, values, v_dtype, old_values, ov_dtype,
+                       returns, r_dtype, cliprange, cliprange_value, vf_coef, lp_out, dhidden, lddh, dh_dtype, dweight,
+                       dw_dtype, lddw, dvalues, workspace, lm_workspace, (hipStream_t)stream);
+}
+
+extern "C" int trlx_ppo_loss_from_hidden_split(
+    const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B, int64_t T, int64_t H, int64_t V,
+    const int64_t* labels, const void* old_lp, int old_dtype, const float* adv0, const float* adv_kl,
+    const float* rew_kl, const float* rew_score, const float* coef, const double* stats8, int unbiased,
+    const double* ctl_state, float kl_coef, float* coef_out, const double* msum, const int64_t* mask,
+    const void* values, int v_dtype, const void* old_values, int ov_dtype, float* rewards, void* returns, int r_dtype,
+    float cliprange, float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh, int dh_dtype,
+    void* dweight, int dw_dtype, int64_t lddw, float* dvalues, void* workspace, void* lm_workspace, void* stream) {
+    LmLossArgs a = {};
+    TRLX_REQUIRE(adv0 && adv_kl && rew_kl && rew_score && rewards, TRLX_ERR_ARG,
+                 "NULL split-beta buffer to trlx_ppo_loss_from_hidden_split");
+    TRLX_REQUIRE((coef != nullptr) != (stats8 != nullptr), TRLX_ERR_ARG,
+                 "trlx_ppo_loss_from_hidden_split: pass exactly one of coef (stored coefficients) and stats8 "
+                 "(the split record the coefficients are derived from)");
+    a.old_lp = old_lp;
+    a.old_dtype = old_dtype;
+    a.adv = adv0;
+    a.adv_kl = adv_kl;
+    a.rew_kl = rew_kl;
+    a.rew_score = rew_score;
+    a.rewards_out = rewards;
+    a.coef = coef;
+    a.wstats = stats8;
+    a.wunbiased = unbiased;
+    a.wctl = ctl_state;
+    a.wbeta = kl_coef;
+    a.coef_out = stats8 ? coef_out : nullptr;
+    a.msum = msum;
+    return ll_ppo_loss(a, hidden, ldh, weight, ldw, B, T, H, V, labels, mask, values, v_dtype, old_values, ov_dtype,
+                       returns, r_dtype, cliprange, cliprange_value, vf_coef, lp_out, dhidden, lddh, dh_dtype, dweight,
+                       dw_dtype, lddw, dvalues, workspace, lm_workspace, (hipStream_t)stream);
 }
 
 extern "C" int trlx_lmhead_logprobs_fwd_saved(const void* hidden, int64_t ldh, const void* weight, int64_t ldw,
@@ -1545,13 +1611,14 @@ extern "C" int trlx_lmhead_logprobs_bwd(const void* hidden, int64_t ldh, const v
     if (N == 0) return TRLX_OK;
     LmLossArgs a = {};
     LlWs w;
-    TRLX_REQUIRE(grad && lse && e && dhidden && dweight, TRLX_ERR_ARG, "NULL grad / lse / E / gradient output");
+    TRLX_REQUIRE(grad && lse && e, TRLX_ERR_ARG, "NULL grad / lse / E");
+    TRLX_REQUIRE(dhidden || dweight, TRLX_ERR_ARG, "neither dhidden nor dweight requested");
     TRLX_REQUIRE(grad_dtype == TRLX_F32 || grad_dtype == TRLX_BF16, TRLX_ERR_DTYPE, "grad dtype");
     TRLX_REQUIRE(dh_dtype == TRLX_BF16 || dh_dtype == TRLX_F32, TRLX_ERR_DTYPE, "dhidden dtype");
     TRLX_REQUIRE(dw_dtype == TRLX_BF16 || dw_dtype == TRLX_F32, TRLX_ERR_DTYPE, "dweight dtype");
     TRLX_REQUIRE(lddh % 4 == 0 && lddh >= H && lddw >= H, TRLX_ERR_STRIDE, "gradient row strides");
     int rc = ll_setup(a, hidden, ldh, weight, ldw, N, H, V, labels, lb, nullptr, lm_workspace, dweight, dw_dtype, lddw,
-                      w, s);
+                      w, s, false);
     if (rc) return rc;
     a.mode = kLLBwd;
     a.gin = grad;
@@ -1563,7 +1630,7 @@ extern "C" int trlx_lmhead_logprobs_bwd(const void* hidden, int64_t ldh, const v
     a.dh_dtype = dh_dtype;
     hipLaunchKernelGGL(k_lmloss_combine<kLLBwd>, dim3(unsigned(N)), dim3(unsigned(H / 4)), 0, s, a);
     rc = check_launch("k_lmloss_combine");
-    if (rc) return rc;
+    if (rc || !dweight) return rc;  // a frozen (or tied elsewhere) lm_head: no dW pass
     return ll_dw_finish(a, dweight, dw_dtype, lddw, w, s);
 }
 

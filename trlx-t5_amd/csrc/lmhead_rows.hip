@@ -668,7 +668,7 @@ using namespace trlx;
 // Round 3: 9 = 128 x 256 tiles, two workgroups per CU (k_lmhead_s2): 0.95x variant 8 at C2's
 // H = 768 (519 vs 544 us), tied at C3, 1.23x slower at H = 4096 (its 32-deep 3-slot ring
 // keeps only ~2 K-steps of DMA in flight; profiles/r03_lmhead_s2_bench.log) -> auto for H <= 1024.
-static thread_local int g_lm_variant = 0;
+static TuneKnob g_lm_variant{0};
 static int lm_variant(int64_t N, int64_t H) {
     if (g_lm_variant) return g_lm_variant;
     return N < 2048 ? 3 : (H <= 1024 ? 9 : 8);

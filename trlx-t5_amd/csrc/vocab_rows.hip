@@ -742,15 +742,15 @@ struct Geometry {
 };
 
 // Tuning knobs (trlx_set_tuning): 0 = automatic.
-static thread_local int g_row_variant = 0;       // 1 = register-resident rows, 2 = streaming rows
-static thread_local int g_resident_threads = 0;  // preferred workgroup size for resident rows
-static thread_local int g_resident_lb512 = 0;    // 1 = <=512-thread rows compiled for 8 waves/SIMD
-static thread_local int g_stream_threads = 0;
-static thread_local int g_stream_unroll = 0;
-static thread_local int g_row_order = 0;         // resident rows: 0 = step-major vectors, 1 = wave-major
-static thread_local int g_ragged_order = 0;      // forward rows with lengths: 0 auto (valid rows first), 1 natural
-static thread_local int g_order_launch = 0;  // ragged order: 0 auto, 1 one launch (k_ragged_order), 2 two (row_order.h)
-static thread_local int g_store_pol = 0;         // gradient-row stores: 0 auto, 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
+static TuneKnob g_row_variant{0};       // 1 = register-resident rows, 2 = streaming rows
+static TuneKnob g_resident_threads{0};  // preferred workgroup size for resident rows
+static TuneKnob g_resident_lb512{0};    // 1 = <=512-thread rows compiled for 8 waves/SIMD
+static TuneKnob g_stream_threads{0};
+static TuneKnob g_stream_unroll{0};
+static TuneKnob g_row_order{0};         // resident rows: 0 = step-major vectors, 1 = wave-major
+static TuneKnob g_ragged_order{0};      // forward rows with lengths: 0 auto (valid rows first), 1 natural
+static TuneKnob g_order_launch{0};  // ragged order: 0 auto, 1 one launch (k_ragged_order), 2 two (row_order.h)
+static TuneKnob g_store_pol{0};         // gradient-row stores: 0 auto, 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
 constexpr double kSC1Bytes = 1.5e9;  // auto: sc1 above this many gradient bytes per launch, else nt
 
 // Cache policy of a launch's gradient-row stores (common.h store_grad_b128).  Measured
@@ -762,10 +762,10 @@ static int store_policy_for(double grad_bytes, bool split) {
     if (g_store_pol) return g_store_pol;
     return (!split && grad_bytes > kSC1Bytes) ? kStoreSC1 : kStoreNT;
 }
-static thread_local int g_split_lds = 0;         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
-static thread_local int g_split_mid = 0;         // mid bf16 rows (loss / backward): 0 auto (= 3), 1 off, 2 5+3, 3 6+2
+static TuneKnob g_split_lds{0};         // long rows: 0 auto (split LDS + VGPR residency), 1 off, 2 also forward
+static TuneKnob g_split_mid{0};         // mid bf16 rows (loss / backward): 0 auto (= 3), 1 off, 2 5+3, 3 6+2
 int tuning_split_lds() { return g_split_lds; }
-static thread_local int g_ilql_split = 0;  // ILQL fp32 split residency: 0 = 20 VGPR + 5 LDS steps, 1 = 22 + 3, 2 = 21 + 4, 3 = 19 + 6
+static TuneKnob g_ilql_split{0};  // ILQL fp32 split residency: 0 = 20 VGPR + 5 LDS steps, 1 = 22 + 3, 2 = 21 + 4, 3 = 19 + 6
 int tuning_ilql_split() { return g_ilql_split; }
 
 // Register-resident geometry: NV (compile-time vectors per thread, from kNVs) and the

@@ -59,17 +59,24 @@ class _LmHeadLogprobs(torch.autograd.Function):
         hshape, hdt, wshape, wdt = ctx.shapes
         N, H, V = h.shape[0], h.shape[1], w.shape[0]
         dev = h.device
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if not (need_h or need_w):
+            return None, None, None, None
         g = grad_lp.reshape(-1).contiguous()
         if g.dtype not in (torch.float32, torch.bfloat16):
             g = g.float()
-        dh = torch.empty((N, H), dtype=hdt, device=dev)
-        dw = torch.empty((V, H), dtype=wdt, device=dev)
-        ws = torch.empty(_lib.query("trlx_lmhead_loss_workspace_bytes", N, H, V), dtype=torch.uint8, device=dev)
+        # a frozen (or tied-and-handled-elsewhere) lm_head skips the dW pass entirely; the
+        # buffers come from PyTorch's stream-ordered caching allocator (no hipMalloc per call
+        # in steady state), and the backward's workspace holds no forward partials
+        dh = torch.empty((N, H), dtype=hdt, device=dev) if need_h else None
+        dw = torch.empty((V, H), dtype=wdt, device=dev) if need_w else None
+        ws = torch.empty(_lib.query("trlx_lmhead_loss_bwd_workspace_bytes", N, H, V), dtype=torch.uint8, device=dev)
         _lib.call("trlx_lmhead_logprobs_bwd", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), N, H, V,
-                  y.data_ptr(), 1, g.data_ptr(), _lib.dtype_code(g), lse.data_ptr(), e.data_ptr(), dh.data_ptr(),
-                  dh.stride(0), _lib.dtype_code(dh), dw.data_ptr(), _lib.dtype_code(dw), dw.stride(0), ws.data_ptr(),
+                  y.data_ptr(), 1, g.data_ptr(), _lib.dtype_code(g), lse.data_ptr(), e.data_ptr(), _lib.ptr(dh),
+                  H if dh is None else dh.stride(0), _lib.dtype_code(dh if dh is not None else dw), _lib.ptr(dw),
+                  _lib.dtype_code(dw if dw is not None else dh), H if dw is None else dw.stride(0), ws.data_ptr(),
                   _lib.stream_of(h))
-        return dh.view(hshape), dw.view(wshape), None, None
+        return (dh.view(hshape) if need_h else None), (dw.view(wshape) if need_w else None), None, None
 
 
 def lm_head_logprobs(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor, out_dtype=None,

@@ -403,13 +403,27 @@ class PPOHotPath:
         scale).  The gemm route keeps a [2, chunk, T, V] bf16 ring (LM_HEAD_CHUNK_TOKENS tokens per
         chunk: the full [2, B, T, V] logits never exist); release_lm_logits() frees it."""
         self._no_pipeline_pending("experience_from_hidden")
+        self._check_hidden(hidden, weight, ref_hidden, ref_weight)
+        labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
+        route = self._lm_route(route, hidden, ref_hidden)
+        s = torch.cuda.current_stream(self.device)
+        if route == "fused":
+            self._launch_pending_tail(s)
+        self._use_split(self.split_beta, 0)
+        g_mom, work = self._begin_step(scores, group, s)
+        self._experience_lmhead(hidden, weight, ref_hidden, ref_weight, labels, lengths, s, route)
+        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
+        return self.lp_old, self.ref_lp
+
+    def _check_hidden(self, hidden, weight, ref_hidden, ref_weight):
         B, T, V = self.B, self.T, self.V
         for h, w in ((hidden, weight), (ref_hidden, ref_weight)):
             if h.dim() != 3 or tuple(h.shape[:2]) != (B, T) or w.dim() != 2 or w.shape[0] != V or \
                     w.shape[1] != h.shape[2] or h.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
                 raise ValueError(f"hidden {tuple(h.shape)}/{h.dtype} and weight {tuple(w.shape)}/{w.dtype} do not "
                                  f"match the hot path ({B},{T},H) x ({V},H) bf16")
-        labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
+
+    def _lm_route(self, route, hidden, ref_hidden):
         if route not in ("auto", "fused", "gemm"):
             raise ValueError(f"route must be auto, fused or gemm, not {route!r}")
         if route == "gemm" and self.dtype != torch.bfloat16:
@@ -417,7 +431,13 @@ class PPOHotPath:
         if route == "auto":
             long_k = min(hidden.shape[2], ref_hidden.shape[2]) >= self.LM_HEAD_GEMM_MIN_H
             route = "gemm" if long_k and self.dtype == torch.bfloat16 else "fused"
-        s = torch.cuda.current_stream(self.device)
+        return route
+
+    def _experience_lmhead(self, hidden, weight, ref_hidden, ref_weight, labels, lengths, s, route):
+        """The policy and reference lm_heads + logprobs into lp_old / ref_lp (the current
+        buffer set): the fused MFMA launches, or hipBLASLt logits over rollout chunks + the
+        experience rows (a deferred loss tail riding the first rows launch)."""
+        B, T, V = self.B, self.T, self.V
         if route == "gemm":
             # rollout chunks: hipBLASLt writes the chunk's policy and reference logits into the
             # ring, one rows launch reads both (the deferred loss tail rides the first)
@@ -425,8 +445,6 @@ class PPOHotPath:
             cb = max(1, min(B, self.LM_HEAD_CHUNK_TOKENS // T))
             if self.lm_logits is None or self.lm_logits.shape[1] != cb:
                 self.lm_logits = torch.empty((2, cb, T, V), dtype=torch.bfloat16, device=self.device)
-            self._use_split(self.split_beta, 0)
-            g_mom, work = self._begin_step(scores, group, s)
             self._ev("experience", s)
             for b0 in range(0, B, cb):
                 nb = min(cb, B - b0)
@@ -436,11 +454,8 @@ class PPOHotPath:
                 self._experience_rows(x0, x1, labels[b0:b0 + nb], s, None if lengths is None else lengths[b0:b0 + nb],
                                       b0=b0, timed=False)
             self._ev_end("experience", s)
-            self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
-            return self.lp_old, self.ref_lp
+            return
         self._launch_pending_tail(s)
-        self._use_split(self.split_beta, 0)
-        g_mom, work = self._begin_step(scores, group, s)
         N = B * T
         nbytes = _lib.query("trlx_lmhead_workspace_bytes", N, V)
         if self.lm_ws is None or self.lm_ws.numel() < nbytes:
@@ -460,8 +475,6 @@ class PPOHotPath:
                 _lib.call("trlx_lmhead_logprobs", h.data_ptr(), h.stride(1), w.data_ptr(), w.stride(0), N, H, V,
                           labels.data_ptr(), 1, out.data_ptr(), _lib.F32, None, self.lm_ws.data_ptr(), s.cuda_stream)
         self._ev_end("experience", s)
-        self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work)
-        return self.lp_old, self.ref_lp
 
     def _experience_tail(self, s, labels, old_values, scores, lengths, mask, group, g_mom, work,
                          defer_allreduce=False, lag=False, launch=True):
@@ -677,8 +690,10 @@ class PPOHotPath:
         :274) without [B, T, V] logits or dlogits in HBM (trlx_ppo_loss_from_hidden: three MFMA
         launches and a per-token combine; tokens with mask == 0 are compacted out).  Returns
         (loss, stats, dhidden [B, T, H], dweight [V, H], dvalues), gradients in grad_dtype;
-        the same loss tail (deferred / side stream) as policy_loss.  Unsplit whitening only (the
-        serial step(): experience / experience_from_hidden, then this).
+        the same loss tail (deferred / side stream) as policy_loss.  After an unsplit GAE (the
+        serial step()) the advantages are whitened by the GAE record; in split-beta mode
+        (pipeline_step_from_hidden, or split_beta=True) by the split record and beta, and the
+        batch's rewards / returns are written here (trlx_ppo_loss_from_hidden_split).
         route: "fused" (the kernels above; H in LOSS_FROM_HIDDEN_SIZES), "gemm" (the
         reference's own structure on the hot path's kernels: hipBLASLt bf16 logits -> the fused
         loss rows (policy_loss) -> hipBLASLt dh = dlogits·W and dW = dlogitsᵀ·h; any H, the
@@ -700,9 +715,6 @@ class PPOHotPath:
         if H not in self.LOSS_FROM_HIDDEN_SIZES:
             raise ValueError(f"policy_loss_from_hidden: fused route not built for hidden size {H} "
                              f"{self.LOSS_FROM_HIDDEN_SIZES} (route='gemm' takes any H)")
-        if self._split_mode:
-            raise RuntimeError("policy_loss_from_hidden runs after the unsplit GAE (step / experience); "
-                               "split-beta / pipelined batches use policy_loss")
         _lib.require_cuda(hidden, weight)
         labels = self._int64(labels, (B, T), "labels")
         mask = self._int64(mask, (B, T), "mask", required=False)
@@ -725,29 +737,50 @@ class PPOHotPath:
         if self.tail_done is not None:
             self.tail_done.wait(s)
         dh, dw = self.dhidden, self.dweight
+        vals = (_lib.ptr(mask), values.data_ptr(), _lib.dtype_code(values), old_values.data_ptr(),
+                _lib.dtype_code(old_values))
+        outs = (float(self.cfg.cliprange), float(self.cfg.cliprange_value), float(self.cfg.vf_coef),
+                self.lp_new.data_ptr(), dh.data_ptr(), H, _lib.dtype_code(dh), dw.data_ptr(), _lib.dtype_code(dw), H,
+                self.dvalues.data_ptr(), self.workspace.data_ptr(), self.lm_loss_ws.data_ptr(), s.cuda_stream)
         self._ev("loss", s)
-        _lib.call("trlx_ppo_loss_from_hidden", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), B, T, H, V,
-                  labels.data_ptr(), self.lp_old.data_ptr(), _lib.F32, self.adv_raw.data_ptr(),
-                  self.adv_stats.data_ptr(), 0 if self.distributed else 1, _lib.ptr(mask), values.data_ptr(),
-                  _lib.dtype_code(values), old_values.data_ptr(), _lib.dtype_code(old_values), self.returns.data_ptr(),
-                  _lib.dtype_code(self.returns), float(self.cfg.cliprange), float(self.cfg.cliprange_value),
-                  float(self.cfg.vf_coef), self.lp_new.data_ptr(), dh.data_ptr(), H, _lib.dtype_code(dh), dw.data_ptr(),
-                  _lib.dtype_code(dw), H, self.dvalues.data_ptr(), self.workspace.data_ptr(),
-                  self.lm_loss_ws.data_ptr(), s.cuda_stream)
+        if self._split_mode:
+            # split beta (the pipelined DP schedule, or step() with split_beta=True): the
+            # whitening coefficients of A = A0 - beta*Ak come from the batch's (all-reduced)
+            # split record and the current beta on the first loss of an experience (stored for a
+            # later one), and this launch writes the batch's rewards and returns — as
+            # trlx_ppo_loss_rows_split_gae does for the logits route
+            sb = self._sbuf[self._sidx]
+            derive = not self._coef_ready
+            _lib.call("trlx_ppo_loss_from_hidden_split", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), B, T,
+                      H, V, labels.data_ptr(), self.lp_old.data_ptr(), _lib.F32, sb["adv0"].data_ptr(),
+                      sb["adv_kl"].data_ptr(), sb["rew_kl"].data_ptr(), sb["rew_score"].data_ptr(),
+                      None if derive else sb["coef"].data_ptr(), sb["stats"].data_ptr() if derive else None,
+                      0 if self.distributed else 1, self.ctl.state.data_ptr() if self.ctl is not None else None,
+                      self.kl_coef, sb["coef"].data_ptr(), sb["stats"].data_ptr() + 6 * 8, *vals,
+                      self.rewards.data_ptr(), self.returns.data_ptr(), _lib.dtype_code(self.returns), *outs)
+            self._coef_ready = True
+            tail_stats = sb["stats"].data_ptr() + 3 * 8  # the tail reads Σmask at stats[3]
+        else:
+            _lib.call("trlx_ppo_loss_from_hidden", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), B, T, H, V,
+                      labels.data_ptr(), self.lp_old.data_ptr(), _lib.F32, self.adv_raw.data_ptr(),
+                      self.adv_stats.data_ptr(), 0 if self.distributed else 1, *vals, self.returns.data_ptr(),
+                      _lib.dtype_code(self.returns), *outs)
+            tail_stats = self.adv_stats.data_ptr()
         self._ev_end("loss", s)
-        self._loss_tail(s, self.adv_stats.data_ptr())
+        self._loss_tail(s, tail_stats)
         return self.loss, self.stats, dh, dw, self.dvalues
 
     def step_from_hidden(self, hidden, weight, ref_hidden, ref_weight, new_hidden, labels, old_values, values,
                          scores, lengths=None, mask=None, group=None, route="auto", new_weight=None,
-                         loss_route="auto"):
+                         loss_route="auto", grad_dtype=torch.bfloat16):
         """step() from hidden states on both sides: experience_from_hidden
         (policy + reference lm_head + logprobs, GAE; `route`) then policy_loss_from_hidden on the
-        updated policy's hidden states (new_weight: its lm_head, default `weight`; `loss_route`)."""
+        updated policy's hidden states (new_weight: its lm_head, default `weight`; `loss_route`,
+        gradients in `grad_dtype`)."""
         self.experience_from_hidden(hidden, weight, ref_hidden, ref_weight, labels, old_values, scores,
                                     lengths=lengths, mask=mask, group=group, route=route)
         return self.policy_loss_from_hidden(new_hidden, weight if new_weight is None else new_weight, labels, values,
-                                            old_values, mask=mask, route=loss_route)
+                                            old_values, mask=mask, route=loss_route, grad_dtype=grad_dtype)
 
     def _policy_loss_from_hidden_gemm(self, hidden, weight, labels, values, old_values, mask, grad_dtype):
         """policy_loss_from_hidden's gemm route: hipBLASLt bf16 logits (the reference's lm_head
@@ -767,9 +800,9 @@ class PPOHotPath:
         if grad_dtype == torch.bfloat16:
             torch.matmul(d2, weight, out=self.dhidden.view(N, H))
             torch.matmul(d2.t(), h2, out=self.dweight)
-        else:
-            self.dhidden.view(N, H).copy_(torch.matmul(d2, weight))
-            self.dweight.copy_(torch.matmul(d2.t(), h2))
+        else:  # bf16 operands, fp32 accumulation AND output (as the fused route's fp32 gradients)
+            self.dhidden.view(N, H).copy_(torch.mm(d2, weight, out_dtype=torch.float32))
+            self.dweight.copy_(torch.mm(d2.t(), h2, out_dtype=torch.float32))
         return loss, stats, self.dhidden, self.dweight, dv
 
     def release_loss_logits(self):
@@ -825,6 +858,57 @@ class PPOHotPath:
         if logits.stride() != ref_logits.stride():
             raise ValueError("policy and reference logits must share strides")
         self._check(new_logits)
+
+        def experience(labels, lengths, s):
+            self._experience_rows(logits, ref_logits, labels, s, lengths)  # + the deferred loss tail(k-1)
+
+        def loss(p, fold):
+            return self.policy_loss(p["new_logits"], p["labels"], p["values"], p["old_values"], mask=p["mask"],
+                                    _fold=fold)
+
+        return self._pipeline(experience, loss, dict(new_logits=new_logits), labels, old_values, values, scores,
+                              lengths, mask, group, fold=self._fold_gae)
+
+    def pipeline_step_from_hidden(self, hidden, weight, ref_hidden, ref_weight, new_hidden, labels, old_values,
+                                  values, scores, lengths: Optional[torch.Tensor] = None,
+                                  mask: Optional[torch.Tensor] = None, group=None, new_weight=None, route="auto",
+                                  loss_route="auto", grad_dtype=torch.bfloat16):
+        """pipeline_step from hidden states on both sides (SURVEY §8f-2 under the data-parallel
+        schedule, accelerate_ppo_model.py:88-126 under the DDP sharding of :146-148): per call
+        (batch k+1)
+
+            E lm_heads(k+1) [loss tail(k-1) first] | [AR(k) in flight beside them]
+              -> GAE(k+1) (split, its own launch) -> join AR(k) -> loss from hidden(k) -> AR(k+1) async
+
+        The loss side of batch k derives its whitening coefficients from the all-reduced split
+        record and beta (trlx_ppo_loss_from_hidden_split), so the whitening all-reduce of batch
+        k hides behind the experience lm_heads of batch k+1 exactly as in pipeline_step, and the
+        results are bit-identical to step_from_hidden on a split_beta=True hot path.  Returns
+        the PREVIOUS batch's (loss, stats, dhidden, dweight, dvalues) or None on the first call
+        (valid until the next call); pipeline_flush() runs the last pending loss.  The GAE keeps
+        its own launch: the loss side is ~2 ms of MFMA work, against which a 7-us launch is
+        noise, and no launch of it can host the rollout waves."""
+        self._check_hidden(hidden, weight, ref_hidden, ref_weight)
+        w_new = weight if new_weight is None else new_weight
+        if tuple(new_hidden.shape[:2]) != (self.B, self.T) or new_hidden.dim() != 3:
+            raise ValueError(f"new_hidden {tuple(new_hidden.shape)} does not match ({self.B},{self.T},H)")
+        route = self._lm_route(route, hidden, ref_hidden)
+
+        def experience(labels, lengths, s):
+            self._experience_lmhead(hidden, weight, ref_hidden, ref_weight, labels, lengths, s, route)
+
+        def loss(p, fold):
+            return self.policy_loss_from_hidden(p["new_hidden"], p["new_weight"], p["labels"], p["values"],
+                                                p["old_values"], mask=p["mask"], grad_dtype=p["grad_dtype"],
+                                                route=p["loss_route"])
+
+        return self._pipeline(experience, loss, dict(new_hidden=new_hidden, new_weight=w_new, grad_dtype=grad_dtype,
+                                                     loss_route=loss_route),
+                              labels, old_values, values, scores, lengths, mask, group, fold=False)
+
+    def _pipeline(self, experience, loss, payload, labels, old_values, values, scores, lengths, mask, group, fold):
+        """The pipelined schedule around an experience launch sequence and a loss (see
+        pipeline_step); fold: the next batch's GAE rides the loss launch (the logits route)."""
         B, T = self.B, self.T
         orig = (labels, lengths, mask)
         labels, lengths, mask, old_values, scores = self._rollout_inputs(labels, lengths, mask, old_values, scores)
@@ -847,29 +931,29 @@ class PPOHotPath:
         self._lag = lag
         g_mom, work = self._begin_step(scores, group, s, lag=lag)  # + AR(k) on the side stream (RCCL, no lag)
         self.lp_old, self.ref_lp = self._lp_bufs[nb]
-        self._experience_rows(logits, ref_logits, labels, s, lengths)  # + the deferred loss tail(k-1)
-        self._resolve_allreduce()  # AR(k): the L rows(k) derive batch k's whitening coefficients from it
+        experience(labels, lengths, s)
+        self._resolve_allreduce()  # AR(k): the loss of batch k derives its whitening coefficients from it
         if lag:  # batch k's all-reduced score moments (none before the first batch)
             g_mom = self._mom_bufs[prev["buf"]] if prev is not None else None
-        # GAE(k+1): its own launch on the first call, else folded into L rows(k)
+        # GAE(k+1): its own launch on the first call (or without folding), else folded into L rows(k)
         gd = self._experience_tail(s, labels, old_values, scores, lengths, mask, group, g_mom, work,
-                                   defer_allreduce=True, lag=lag, launch=prev is None or not self._fold_gae)
+                                   defer_allreduce=True, lag=lag, launch=prev is None or not fold)
         out = None
         if prev is not None:
             self._use_split(True, prev["buf"])
             self.lp_old, self.ref_lp = self._lp_bufs[prev["buf"]]
-            out = self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
-                                   mask=prev["mask"], _fold=gd if self._fold_gae else None)
+            out = prev["loss"](prev, gd if fold else None)
             self._use_split(True, nb)
             self.lp_old, self.ref_lp = self._lp_bufs[nb]
-            if self._fold_gae:
+            if fold:
                 self._gae_done(gd, s)
-        self._pending = dict(buf=nb, new_logits=new_logits, labels=labels, values=values, old_values=old_values,
+        self._pending = dict(payload, buf=nb, loss=loss, labels=labels, values=values, old_values=old_values,
                              mask=mask)
         return out
 
     def pipeline_flush(self):
-        """Run the pending loss of the last pipeline_step batch; returns its outputs (or None)."""
+        """Run the pending loss of the last pipeline_step(_from_hidden) batch; returns its outputs
+        (or None)."""
         prev, self._pending = self._pending, None
         if prev is None:
             return None
@@ -881,8 +965,7 @@ class PPOHotPath:
             _lib.call("trlx_score_moments_merge", st, st, self._mom_bufs[prev["buf"]].data_ptr(),
                       torch.cuda.current_stream(self.device).cuda_stream)
             self._lag = False
-        return self.policy_loss(prev["new_logits"], prev["labels"], prev["values"], prev["old_values"],
-                                mask=prev["mask"])
+        return prev["loss"](prev, None)
 
     def step(self, logits, ref_logits, new_logits, labels, old_values, values, scores,
              lengths: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, group=None,
