@@ -59,6 +59,13 @@ for step in "$@"; do
                      -o run -- python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --no-timers ;;
         newtests) run new_tests 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread -p no:cacheprovider \
                      tests/test_gpu_lmhead_loss.py tests/test_gpu_dist_hidden.py tests/test_gpu_dist_world.py ;;
+        hstests) run hs_tests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+                     tests/test_gpu_lmhead_loss.py -k "h_sliced" ;;
+        forms) run forms_c2 300 python tools/lmloss_forms.py --config c2 --fwd 1,2,3,4 --dw 1,2,3 &&
+               run forms_c3 300 python tools/lmloss_forms.py --config c3 --fwd 1,2,4 --dw 1,3 ;;
+        stamps) LL_HS=1 LL_STAMPS=1 LL_TUNE=lmloss_fwd=4,lmloss_dw=3 run stamps 300 python tools/lmloss_ablate.py --libs stamp/lib_stamp.so ;;
+        ablate) LL_HS=1 LL_STAMPS=1 LL_TUNE=lmloss_fwd=3,lmloss_dw=2 run ablate 300 python tools/lmloss_ablate.py \
+                    --libs stamp/lib_stamp.so,stamp/lib_abl4.so,stamp/lib_abl1.so ;;
         bench20) run bench20 400 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac

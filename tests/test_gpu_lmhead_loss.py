@@ -454,3 +454,100 @@ def test_hot_path_loss_side_halves(B, T, V, H, masked, kind):
                             e64[live.to(DEV)], fp32_out=True))
     C.assert_within(errs, f"hot path {kind} B={B} V={V} masked={masked}")
     assert (dh.reshape(N, H)[~live.to(DEV)] == 0).all()
+
+
+@pytest.mark.parametrize("kind,N,H,V", [("flat", 6144, 768, 50257), ("peaked", 6144, 768, 50257),
+                                        ("peaked", 2000, 768, 32128), ("flat", 333, 768, 1031),
+                                        ("peaked", 1000, 512, 5000), ("flat", 70, 512, 33), ("flat", 17, 768, 100)])
+@pytest.mark.parametrize("fwd,dw", [(3, 2), (1, 2), (3, 1), (4, 3)])
+def test_lm_head_loss_h_sliced_forms(kind, N, H, V, fwd, dw):
+    """The H-sliced forms (tunings lmloss_fwd = 3, lmloss_dw = 2: each wave owns a quarter of
+    the hidden dimension for its 64 register rows, 16-row tiles, one barrier per tile) against
+    fp64 with the halves checks — ragged token counts (17, 70, 333: partial 16-token tiles and
+    64-token blocks), vocab sizes off the 16-row tile (33, 100, 1031, 50257) and both hidden
+    sizes."""
+    h, w, y = _halves_operands(kind, N, H, V, 7 * N + V)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(17))
+    t = C.fp64_truth(h.to(DEV), w.to(DEV), y.to(DEV), gout.to(DEV))
+    P._lib.set_tuning("lmloss_fwd", fwd)
+    P._lib.set_tuning("lmloss_dw", dw)
+    try:
+        for dh_dt, dw_dt in ((torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)):
+            lp, lse, e, dh, dwt = _fwd_saved_bwd(h, w, y, gout, dh_dt, dw_dt)
+            torch.testing.assert_close(lp.double(), t["lp"], rtol=1e-5, atol=2e-5)
+            torch.testing.assert_close(lse.double(), t["lse"], rtol=1e-6, atol=2e-5)
+            errs = C.e_errors(e, t["e"])
+            errs.update(C.dw_errors(dwt, t["dw"], y))
+            errs.update(C.dh_errors(dh, t["dh"], gout, t["e"], fp32_out=dh_dt == torch.float32))
+            C.assert_within(errs, f"H-sliced fwd={fwd} dw={dw} {kind} N={N} H={H} V={V} out={dh_dt}")
+    finally:
+        P._lib.set_tuning("lmloss_fwd", 0)
+        P._lib.set_tuning("lmloss_dw", 0)
+
+
+@pytest.mark.parametrize("fwd,dw", [(3, 2), (4, 3)])
+@pytest.mark.parametrize("splits,tsplit", [(1, 1), (3, 2), (8, 5), (5, 16)])
+def test_lm_head_loss_h_sliced_plans(splits, tsplit, fwd, dw):
+    """Forced grid plans on the H-sliced forms: vocab splits of the forward, token splits of
+    the dW kernel's last round (fp32 partials + the fixed-order reduce), and the restart of
+    the fixed-offset softmax (a logit jump of ~80 from the 3rd tile on)."""
+    N, H, V = 200, 768, 7000
+    for jump in (False, True):
+        h, w, y = _operands(N, H, V, 5 + jump)
+        if jump:
+            wf = w.float()
+            dvec = h.float().mean(0)
+            wf[2 * 16:] += 80.0 * dvec / (dvec @ dvec)
+            w = wf.to(torch.bfloat16)
+        gout = torch.randn(N, generator=torch.Generator().manual_seed(6))
+        t = C.fp64_truth(h.to(DEV), w.to(DEV), y.to(DEV), gout.to(DEV))
+        P._lib.set_tuning("lmloss_fwd", fwd)
+        P._lib.set_tuning("lmloss_dw", dw)
+        P._lib.set_tuning("lmloss_splits", splits)
+        P._lib.set_tuning("lmloss_dw_tsplit", tsplit)
+        try:
+            lp, lse, e, dh, dwt = _fwd_saved_bwd(h, w, y, gout, torch.float32, torch.float32)
+        finally:
+            for k in ("lmloss_fwd", "lmloss_dw", "lmloss_splits", "lmloss_dw_tsplit"):
+                P._lib.set_tuning(k, 0)
+        assert torch.isfinite(lp).all() and torch.isfinite(dh).all()
+        torch.testing.assert_close(lp.double(), t["lp"], rtol=1e-5, atol=1e-4)
+        errs = C.e_errors(e, t["e"])
+        errs.update(C.dw_errors(dwt, t["dw"], y))
+        errs.update(C.dh_errors(dh, t["dh"], gout, t["e"], fp32_out=True))
+        C.assert_within(errs, f"H-sliced plans splits={splits} tsplit={tsplit} jump={jump}")
+
+
+@pytest.mark.parametrize("B,T,V,H,masked", [(128, 48, 50257, 768, False), (256, 48, 32128, 768, True),
+                                            (8, 20, 5000, 512, True)])
+def test_hot_path_h_sliced_matches_row_split(B, T, V, H, masked):
+    """The PPO route (compaction of masked tokens, the PPO combine) on the H-sliced forms
+    against the row-split forms on the same step: loss, stats and dvalues equal to fp32
+    summation order, dh / dW to the bf16 rounding of P / dS."""
+    x = _ppo_inputs(B, T, V, H, 900 + B, masked)
+    d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in x.items()}
+    if masked:
+        d["new_h"] = d["new_h"].masked_fill((d["mask"] == 0)[..., None], float("nan"))
+    outs = {}
+    for fwd, dw in ((1, 1), (3, 2), (4, 3)):
+        P._lib.set_tuning("lmloss_fwd", fwd)
+        P._lib.set_tuning("lmloss_dw", dw)
+        try:
+            hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
+            o = hp.step_from_hidden(d["h"], d["w"], d["ref_h"], d["w"], d["new_h"], d["labels"], d["old_values"],
+                                    d["values"], d["scores"], lengths=d["lengths"], mask=d["mask"], route="fused",
+                                    loss_route="fused", grad_dtype=torch.float32)
+            torch.cuda.synchronize()
+            outs[fwd] = [t.clone() for t in o] + [hp.lp_new.clone()]
+        finally:
+            P._lib.set_tuning("lmloss_fwd", 0)
+            P._lib.set_tuning("lmloss_dw", 0)
+    a = outs[1]
+    for f in (3, 4):
+        b = outs[f]
+        torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(b[1], a[1], rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(b[4], a[4], rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(b[5], a[5], rtol=1e-5, atol=1e-5)
+        assert _rel(b[2], a[2]) < 4e-3 and _rel(b[3], a[3]) < 4e-3
+        assert torch.isfinite(b[2]).all() and torch.isfinite(b[3]).all()

@@ -65,6 +65,16 @@ def child(N, H, V, iters):
         lib = L.load()
         lib.trlx_debug_ll_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         assert lib.trlx_debug_ll_stamps(buf.ctypes.data, buf.size) == 0
+        if os.environ.get("LL_HS"):  # H-sliced engine: [wait+barrier, S part, P part, phases] per wave
+            for name, reg in (("fwd_hs", buf[:1 << 15]), ("dw_hs", buf[1 << 15:])):
+                m = reg.reshape(-1, 8)
+                m = m[m[:, 3] > 0].astype(np.float64)
+                if m.size:
+                    per = m[:, :3] / m[:, 3:4]
+                    out[name + "_stamp_cycles_per_phase"] = {n: round(float(v), 1) for n, v in zip(
+                        ["wait_dma+barrier", "S_part(+X)", "P_part"], per.mean(0))}
+                    out[name + "_phases_per_wave"] = float(m[:, 3].mean())
+            buf[:] = 0
         dm = buf[1 << 15:].reshape(-1, 8)
         dm = dm[dm[:, 6] > 0].astype(np.float64)
         if dm.size:
@@ -73,7 +83,7 @@ def child(N, H, V, iters):
                 ["wait_dma+barrier", "S_phase", "dS_tail", "dW_phase"], dper.mean(0))}
         sm = buf[:1 << 15].reshape(-1, 8)
         sm = sm[sm[:, 6] > 0].astype(np.float64)
-        per = sm[:, :6] / sm[:, 6:7]
+        per = sm[:, :6] / sm[:, 6:7] if sm.size else np.zeros((1, 6))
         names = ["wait_dma+barrier", "S+softmax", "xwrite+dma_issue", "O_product", "mid_barrier", "xread"]
         out["stamp_cycles_per_step"] = {n: round(float(v), 1) for n, v in zip(names, per.mean(0))}
         out["stamp_waves"] = int(sm.shape[0])

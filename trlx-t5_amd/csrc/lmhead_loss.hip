@@ -1266,22 +1266,988 @@ __global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int
     }
 }
 
+// ------------------------------------------------------------------ H-sliced forms (round 5)
+// Both MFMA kernels as ONE engine whose four waves split the hidden dimension instead of the
+// rows: wave q owns hidden columns [q·HS, (q+1)·HS), HS = H/4, for its register operand (64
+// rows x HS: 96 registers at H = 768) AND its accumulators (64 rows x HS fp32: 192), and the
+// workgroup streams 16-row tiles of the other operand through a 4-slot LDS ring:
+//   dW:      registers = W rows v0..v0+63,  tiles = h (16 tokens),  accumulators = dWᵀ
+//   forward: registers = h rows m0..m0+63,  tiles = W (16 vocab),   accumulators = Oᵀ
+// Per tile: the partial S over the wave's slice (16x16x32: M = the 16 tile rows, N = 4 blocks
+// of 16 register rows, K = 32 hidden columns — every row fragment read from LDS feeds 4 MFMAs),
+// the four partials summed through LDS by the wave that owns register block q (fixed order
+// w = 0..3), its X step — dS = g·(1[y = v] − p) (dW) or P = exp(S − offset) (forward) — into a
+// bf16 [64 register rows][16 tile rows] image, and the second product (32x32x16: M = 32 hidden
+// columns, N = 32 register rows, K = the 16 tile rows; the tile read transposed, each fragment
+// feeding 2 MFMAs).  Against the row-split forms (k_lmloss_dw: a wave per 16 vocab rows over
+// the whole H, every tile fragment feeding ONE MFMA) this reads a quarter of the tile bytes
+// from LDS per MFMA, which was the dW kernel's bound.
+// The step is pipelined three tiles deep with ONE barrier per tile:
+//   phase t:  MFMA S(t) [rows of tile t] + MFMA P(t-2) [tile t-2 transposed, X(t-2)]
+//             VALU X(t-1) [partials of S(t-1) -> X image]; writes S(t) partials; DMA tile t+1
+// so a phase's barrier publishes S(t-1)'s partials, X(t-2)'s image and tile t's bytes at
+// once.  LDS: 4 tile slots (24 KB at H = 768, + 1 KB of token records for dW), 2 partial
+// buffers (16 KB: [writer][block][lane] f32x4), 2 X images (2 KB) = 136 KB.
+// Tile image: two 8-row groups of [8 rows][H] in 512-B subtiles (8 rows x 32 columns), the
+// 16-B chunk slot XOR-swizzled by ll16_swz((row>>2)&3): conflict-free for the 16x16x32 row
+// reads and the 32x32x16 transposed reads (MI355X_MICROARCH.md LDS banking), and every read of
+// a wave is one of three lane bases plus an immediate (512 B per 32-column group).
+template <int H_>
+struct HsG {
+    static constexpr int H = H_, HS = H / 4, KS = HS / 32, CB = HS / 32;
+    static constexpr int kRows = 16, kTile = kRows * H * 2;
+    static constexpr int kPieces = kTile / 1024, NI = kPieces / 4, NPR = H / 64;
+    static constexpr int kRowGroup = 8 * H * 2;
+    static constexpr int kSlot = kTile + 1024;
+    static constexpr int kXBuf = 16 * 1024;
+    static constexpr int kXs = 64 * 32;
+    static constexpr int kLds = 4 * kSlot + 2 * kXBuf + 2 * kXs;
+    static_assert(kPieces % 4 == 0 && NI == KS && kLds <= 163840, "H-sliced geometry");
+};
+
+// the tile row lane `lane` of DMA piece i fills, and its source chunk (16 B units of the row)
+template <class G>
+__device__ __forceinline__ int hs_piece_row(int i, int lane) {
+    return 8 * (i / G::NPR) + ((lane >> 2) & 7);
+}
+template <class G>
+__device__ __forceinline__ int hs_piece_chunk(int i, int lane) {
+    const int r = hs_piece_row<G>(i, lane);
+    const int u = 2 * (i % G::NPR) + (lane >> 5);
+    return 4 * u + ((lane & 3) ^ ll16_swz((r >> 2) & 3));
+}
+// lane bases: row read (16x16x32 operand: tile row lane&15, chunk 4u + (lane>>4)) and the two
+// halves of a transposed read (32x32x16 operand: column lane&31 of a 32-column group, tile
+// rows 8(lane>>5) + 4·half + 0..3)
+template <class G>
+__device__ __forceinline__ int hs_rb(int lane) {
+    const int g = lane >> 4, c = lane & 15;
+    return (c >> 3) * G::kRowGroup + 64 * (c & 7) + 16 * (g ^ ll16_swz((c >> 2) & 3));
+}
+template <class G>
+__device__ __forceinline__ int hs_trb(int lane, int half) {
+    const int G4 = lane >> 4, qq = (lane >> 2) & 3, p = lane & 3;
+    const int r = 8 * (G4 >> 1) + 4 * half + qq;
+    return (G4 >> 1) * G::kRowGroup + 64 * (r & 7) + 16 * ((2 * (G4 & 1) + (p >> 1)) ^ ll16_swz((r >> 2) & 3)) +
+           8 * (p & 1);
+}
+__device__ __forceinline__ bf16x8_t hs_row(const char* tile, int rb, int u) {
+    return *reinterpret_cast<const bf16x8_t*>(tile + rb + 512 * u);
+}
+__device__ __forceinline__ bf16x8_t hs_tr(const char* tile, int trb0, int trb1, int u) {
+    typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(tile + trb0 + 512 * u));
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(tile + trb1 + 512 * u));
+    const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    return __builtin_bit_cast(bf16x8_t, v);
+}
+// X image [64 register rows][16 tile rows] bf16, 32 B a row, the 16-B halves swapped on rows
+// with bit 3 set: the B-operand read (row 32b + lane&31, tile rows 8(lane>>5)..+7) is
+// conflict-free.
+__device__ __forceinline__ int hs_xs_rd(int lane) {
+    const int r = lane & 31;
+    return r * 32 + 16 * ((lane >> 5) ^ ((r >> 3) & 1));
+}
+__device__ __forceinline__ int hs_xs_wr(int q, int g, int c) {
+    return (16 * q + c) * 32 + 16 * ((g >> 1) ^ ((c >> 3) & 1)) + 8 * (g & 1);
+}
+
+enum { kHsDw = 0, kHsFwd = 1 };
+
+// One 1-KB LDS-DMA piece as an asm statement (cdna_hip_programming.md §5.7: M0 written and
+// restored inside it): hipcc does not model it, so it inserts no wait for the LDS reads still
+// in flight when a piece is issued (the builtin form drew an lgkmcnt wait for every older
+// ds_read before each piece: the compiler cannot tell the landing slot from the slots being
+// read) — the engine waits for its own pieces with vmcnt(0) at the next phase.
+__device__ __forceinline__ void hs_dma(__amdgpu_buffer_rsrc_t rs, const char* lds, int voff) {
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        uint32_t(uintptr_t((const __attribute__((address_space(3))) char*)lds)));
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(dst), "s"(rs)
+                 : "memory");
+}
+
+// The engine.  ROLE kHsDw: rop = W fragments, the grid / token split of k_lmloss_dw; the
+// caller stores acc2 as dWᵀ rows.  ROLE kHsFwd: rop = h fragments of token block m0, the vocab
+// tiles [t0, t1) of one split; fixed exponent offset per token = its first tile's max
+// (overflow -> the RESTART launch, as ll_fwd_block).  Returns through acc2 (+ the forward's
+// per-token state in fs).
+struct HsFwdState {
+    float mfix, mtrue, lrun;
+    bool bad;
+};
+
+template <class G, int ROLE, bool RESTART>
+__device__ __forceinline__ void hs_engine(const LmLossArgs& a, char* smem, const bf16x8_t (&rop)[4][G::KS],
+                                          f32x16_t (&acc2)[2][G::CB], int t0, int t1, int q, int v0, int nv,
+                                          HsFwdState& fs) {
+    constexpr int KS = G::KS, CB = G::CB, NI = G::NI;
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, c = lane & 15;
+    const int u0 = q * (G::HS / 32);  // the wave's first 32-column group
+    char* slots = smem;
+    char* xbuf = smem + 4 * G::kSlot;
+    char* xsb = xbuf + 2 * G::kXBuf;
+    const int rb = hs_rb<G>(lane), trb0 = hs_trb<G>(lane, 0), trb1 = hs_trb<G>(lane, 1);
+    const int xsr = hs_xs_rd(lane), xsw = hs_xs_wr(q, g, c);
+    // ---- DMA sources
+    const __amdgpu_buffer_rsrc_t rsrc =
+        ROLE == kHsDw ? make_rsrc(a.h, uint32_t(int64_t(a.N) * a.ldh * 2)) : make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
+    const int ld2 = ROLE == kHsDw ? int(a.ldh) * 2 : int(a.ldw) * 2;
+    const __amdgpu_buffer_rsrc_t rrec = make_rsrc(a.trec, uint32_t(a.N) * 16u);
+    const __amdgpu_buffer_rsrc_t rrows = make_rsrc(a.rows, a.rows ? uint32_t(a.N) * 4u : 0u);
+    // dW: a lane's two source rows (tile rows (l>>2)&7 and 8 + that) of the next tile, by index
+    // loads one tile ahead (compacted tokens); past the live tokens row N (zero fill)
+    const int rA = (lane >> 2) & 7;
+    auto tok_row = [&](int m) __attribute__((always_inline)) { return m < nv ? (a.rows ? a.rows[m] : m) : a.N; };
+    int nrowA = 0, nrowB = 0;  // dW, compacted: the row indices of tile t+1, loaded during phase t-1
+    auto piece = [&](int t, char* slot, int k, int rowa, int rowb) __attribute__((always_inline)) {
+        const int i = q + 4 * k;
+        const int r = hs_piece_row<G>(i, lane);
+        int rbytes;
+        if (ROLE == kHsDw)
+            rbytes = int(__umul24(uint32_t(r < 8 ? rowa : rowb), uint32_t(ld2)));
+        else
+            rbytes = (t * 16 + r) * ld2;
+        const int off = rbytes + 16 * hs_piece_chunk<G>(i, lane);
+        hs_dma(rsrc, slot + i * 1024, t < t1 ? off : int(0x7ffff000));
+    };
+    auto records = [&](int t, char* slot) __attribute__((always_inline)) {  // dW: 16 tokens' {-lse·log2e, g, y}
+        const int m = t * 16 + (lane & 15);
+        hs_dma(rrec, slot + G::kTile, t < t1 && m < nv ? m * 16 : int(0x7ffffff0));
+    };
+    f32x4_t acc[4];
+#if LL_STAMP
+    unsigned long long hst[4] = {};  // steady phases: wait + barrier, S part, P part, count
+    unsigned long long hts0 = 0, hts1 = 0;
+#endif
+    // ---- one phase (FL bit 1: S(t), 2: X(t-1), 4: P(t-2)); LDS regions as restrict parameters
+    auto body = [&](auto fl_tag, int t, const char* __restrict__ cur, const char* __restrict__ old,
+                    const char* __restrict__ prv, char* __restrict__ nxt, char* __restrict__ xw,
+                    const char* __restrict__ xr, char* __restrict__ xsw_p, const char* __restrict__ xsr_p)
+                    __attribute__((always_inline)) {
+        constexpr int FL = decltype(fl_tag)::value;
+        constexpr bool DS = FL & 1, DX = FL & 2, DP = FL & 4;
+        constexpr int NGS = DS ? 4 * KS : 0, NGP = DP ? 2 * CB : 0, NG = NGS + NGP;
+        // dW: this phase's DMA takes tile t+1's rows (row N past the live tokens: zero fill);
+        // the index loads fetch tile t+2's (unconditional, picked next phase: a load under a
+        // branch made hipcc wait for it at the join)
+        int pa = 0, pb = 0;
+        if (ROLE == kHsDw && DS) {
+            const int ma = (t + 1) * 16 + rA, mb = ma + 8;
+            pa = ma < nv ? (a.rows ? nrowA : ma) : a.N;
+            pb = mb < nv ? (a.rows ? nrowB : mb) : a.N;
+            nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 2) * 16 + rA, nv - 1) * 4, 0, 0);
+            nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 2) * 16 + 8 + rA, nv - 1) * 4, 0, 0);
+        }
+        // LDS reads in the order of first use (LDS returns in order: a read waits for every
+        // older one): S(t)'s first row fragments, X(t-2)'s operand, S(t-1)'s partials, records
+        constexpr int PF = 3;
+        bf16x8_t rf[KS];
+        if (DS) {
+#pragma unroll
+            for (int ks = 0; ks < PF && ks < KS; ++ks) rf[ks] = hs_row(cur, rb, u0 + ks);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[b] = f32x4_t{};
+        }
+        bf16x8_t xsf[2];
+        if (DP) {
+            xsf[0] = *reinterpret_cast<const bf16x8_t*>(xsr_p + xsr);
+            xsf[1] = *reinterpret_cast<const bf16x8_t*>(xsr_p + xsr + 1024);
+        }
+        f32x4_t xv[4];
+        f32x4_t rec[4];
+        if (DX) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) xv[w] = reinterpret_cast<const f32x4_t*>(xr + (w * 4 + q) * 1024)[lane];
+            if (ROLE == kHsDw) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) rec[r] = *reinterpret_cast<const f32x4_t*>(prv + G::kTile + 16 * (4 * g + r));
+            }
+        }
+        bf16x8_t tf[CB];
+        float s[4], xo[4];
+        // X chunks: 0 sum, 1 (fwd) token max, 2 offset, 3 exp + pack (dW: 1 exp + dS, 2 pack)
+        // X(t-1) in eight micro-steps of at most ~5 vector instructions (one transcendental
+        // pair), one per MFMA gap of the P part (32-cycle gaps leave ~24 cycles of issue each;
+        // MI355X_MICROARCH.md 'vector-instruction ISSUE cost'), the image store in the last.
+        auto xmicro = [&](int m) __attribute__((always_inline)) {
+            if (kLLAblate & 1) return;
+            const int tp = t - 1;
+            if (m < 2) {
+#pragma unroll
+                for (int r = 2 * m; r < 2 * m + 2; ++r) s[r] = ((xv[0][r] + xv[1][r]) + xv[2][r]) + xv[3][r];
+                return;
+            }
+            if (ROLE == kHsDw) {
+                if (m == 2 || m == 3) {
+#pragma unroll
+                    for (int r = 2 * (m - 2); r < 2 * (m - 2) + 2; ++r) {
+                        asm volatile("" ::"v"(rec[r]));  // the whole 16-B record live until here: no WAW
+                                                         // stall on its unused word
+                        xo[r] = exp2_fast(fmaf(s[r], kLog2e, rec[r].x));
+                    }
+                } else if (m == 4 || m == 5) {
+                    const int vcol = v0 + 16 * q + c;
+#pragma unroll
+                    for (int r = 2 * (m - 4); r < 2 * (m - 4) + 2; ++r) {
+                        const float gv = rec[r].y;
+                        xo[r] = fmaf(-gv, xo[r], __float_as_int(rec[r].z) == vcol ? gv : 0.0f);
+                    }
+                } else if (m == 6) {
+                    *reinterpret_cast<uint2*>(xsw_p + xsw) = make_uint2(pack_bf2(xo[0], xo[1]), pack_bf2(xo[2], xo[3]));
+                }
+            } else {
+                if (m == 2) {
+                    if ((tp + 1) * 16 > a.V) {  // the vocab's last tile (wave-uniform): rows past V
+                        const int lim = a.V - tp * 16 - 4 * g;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) s[r] = r < lim ? s[r] : -INFINITY;
+                    }
+                    xo[0] = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+                } else if (m == 3) {
+                    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(xo[0]), __float_as_uint(xo[0]),
+                                                                     false, false);
+                    xo[0] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));  // lanes l, l^16
+                } else if (m == 4) {
+                    const float mx = ll_pair_max(xo[0]);  // lanes l, l^32: the token's 16 tile rows
+                    if (!RESTART) {
+                        fs.mtrue = fmaxf(fs.mtrue, mx);
+                        fs.mfix = tp == t0 ? mx : fs.mfix;
+                        fs.bad = fs.bad || mx > fs.mfix + kLLOverflow;
+                    }
+                    xo[1] = -fs.mfix * kLog2e;
+                } else if (m == 5 || m == 6) {
+                    const float nm = xo[1];
+#pragma unroll
+                    for (int r = 2 * (m - 5); r < 2 * (m - 5) + 2; ++r) s[r] = exp2_fast(fmaf(s[r], kLog2e, nm));
+                } else if (m == 7) {
+                    fs.lrun += (s[0] + s[1]) + (s[2] + s[3]);
+                    *reinterpret_cast<uint2*>(xsw_p + xsw) = make_uint2(pack_bf2(s[0], s[1]), pack_bf2(s[2], s[3]));
+                }
+            }
+        };
+        constexpr int NXM = 8;
+        // where micro-step m runs: P gap XJ0 + m; without a P part, the last 8 S gaps; without
+        // either, straight after the loop
+        constexpr int XJ0 = 2 * CB >= NXM + 1 ? 1 : 0;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            if (k < NGS) {
+                const int ks = k >> 2, b = k & 3;
+                if (b == 0 && ks + PF < KS) rf[ks + PF] = hs_row(cur, rb, u0 + ks + PF);
+                acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rf[ks], rop[b][ks], acc[b], 0, 0, 0);
+                if ((k & 3) == 1 && (k >> 2) < NI && !(kLLAblate & 4)) {
+                    piece(t + 1, nxt, k >> 2, pa, pb);
+                    if (ROLE == kHsDw && q == 0 && (k >> 2) == 0) records(t + 1, nxt);
+                }
+                if (DP && k >= NGS - 6 && ((NGS - k) & 1) == 0 && (NGS - k) / 2 <= 3)  // tf[0..2], 2 gaps apart
+                    tf[3 - (NGS - k) / 2] = hs_tr(old, trb0, trb1, u0 + 3 - (NGS - k) / 2);
+            } else if (k < NG) {
+                const int j = k - NGS, cb = j >> 1, b2 = j & 1;
+                if (!DS && j == 0) {
+#pragma unroll
+                    for (int x = 0; x < 3 && x < CB; ++x) tf[x] = hs_tr(old, trb0, trb1, u0 + x);
+                }
+                if (b2 == 0 && cb + 3 < CB) tf[cb + 3] = hs_tr(old, trb0, trb1, u0 + cb + 3);
+                acc2[b2][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[cb], xsf[b2], acc2[b2][cb], 0, 0, 0);
+                if (DS && j >= 1 && j <= 4)  // S(t)'s partials (their MFMAs done)
+                    reinterpret_cast<f32x4_t*>(xw + (q * 4 + (j - 1)) * 1024)[lane] = acc[j - 1];
+            }
+            if (DX) {
+                constexpr int XK0 = DP ? NGS + XJ0 : NGS - NXM;
+#pragma unroll
+                for (int m = 0; m < NXM; ++m)
+                    if (k == XK0 + m) xmicro(m);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#if LL_STAMP
+            if (FL == 7 && k == NGS - 1) {
+                unsigned long long tsx = 0;
+                LL_TS(tsx);
+                hst[1] += tsx - hts1;
+                hts1 = tsx;
+            }
+#endif
+        }
+#if LL_STAMP
+        if (FL == 7) {
+            unsigned long long tsx = 0;
+            LL_TS(tsx);
+            hst[2] += tsx - hts1;
+            hst[3] += 1;
+        }
+#endif
+        if (DS && !DP) {  // no P MFMAs to carry them: S(t)'s partials now
+#pragma unroll
+            for (int b = 0; b < 4; ++b) reinterpret_cast<f32x4_t*>(xw + (q * 4 + b) * 1024)[lane] = acc[b];
+        }
+        if (DX && NG == 0) {
+#pragma unroll
+            for (int m = 0; m < NXM; ++m) xmicro(m);
+        }
+    };
+    auto phase = [&](auto fl_tag, int t) __attribute__((always_inline)) {
+#if LL_STAMP
+        LL_TS(hts0);
+#endif
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t (and the index loads)
+        ll_lds_barrier();                          // everyone's: tile t, S(t-1) partials, X(t-2)
+#if LL_STAMP
+        LL_TS(hts1);
+        if (decltype(fl_tag)::value == 7) hst[0] += hts1 - hts0;
+#endif
+        body(fl_tag, t, slots + (t & 3) * G::kSlot, slots + ((t - 2) & 3) * G::kSlot,
+             slots + ((t - 1) & 3) * G::kSlot, slots + ((t + 1) & 3) * G::kSlot, xbuf + (t & 1) * G::kXBuf,
+             xbuf + ((t - 1) & 1) * G::kXBuf, xsb + ((t - 1) & 1) * G::kXs, xsb + ((t - 2) & 1) * G::kXs);
+    };
+    if (t0 >= t1) return;
+    {  // prologue: tile t0's DMA
+        char* s0 = slots + (t0 & 3) * G::kSlot;
+        const int ra0 = ROLE == kHsDw ? tok_row(t0 * 16 + rA) : 0, rb0 = ROLE == kHsDw ? tok_row(t0 * 16 + 8 + rA) : 0;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) piece(t0, s0, k, ra0, rb0);
+        if (ROLE == kHsDw && q == 0) records(t0, s0);
+        if (ROLE == kHsDw && a.rows) {  // tile t0+1's row indices
+            nrowA = a.rows[min((t0 + 1) * 16 + rA, nv - 1)];
+            nrowB = a.rows[min((t0 + 1) * 16 + 8 + rA, nv - 1)];
+        }
+    }
+    using F1 = std::integral_constant<int, 1>;
+    using F3 = std::integral_constant<int, 3>;
+    using F7 = std::integral_constant<int, 7>;
+    using F6 = std::integral_constant<int, 6>;
+    using F2 = std::integral_constant<int, 2>;
+    using F4 = std::integral_constant<int, 4>;
+    phase(F1{}, t0);
+    if (t0 + 1 < t1) {
+        phase(F3{}, t0 + 1);
+        for (int t = t0 + 2; t < t1; ++t) phase(F7{}, t);
+        phase(F6{}, t1);
+    } else {
+        phase(F2{}, t1);
+    }
+    phase(F4{}, t1 + 1);
+#if LL_STAMP
+    {  // per wave: fwd at [0, 2^15), dW at [2^15, 2^16) of g_ll_stamps, 8 words a wave
+        const int slot = int(blockIdx.x) * 4 + q;
+        if (lane == 0 && slot < (1 << 12))
+            for (int k = 0; k < 4; ++k) g_ll_stamps[(ROLE == kHsDw ? (1 << 15) : 0) + slot * 8 + k] = hst[k];
+    }
+#endif
+}
+
+// dW, H-sliced: per 64-row vocab block (or, in the last partial round, a token split of one:
+// the plan of k_lmloss_dw), the engine over the block's 16-token tiles of h, then dWᵀ rows:
+// lane l holds vocab row v0 + 32b + (l&31) at 16 columns in runs of 4 (f32x4 / 8-B stores).
+template <class G>
+__global__ __launch_bounds__(256, 1) void k_lmloss_dw_hs(LmLossArgs a) {
+    constexpr int KS = G::KS, CB = G::CB, HS = G::HS;
+    __shared__ __attribute__((aligned(16))) char smem[G::kLds];
+    const int lane = threadIdx.x & 63;
+    const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, c = lane & 15;
+    const int nv = a.rows ? *a.nrows : a.N;
+    const bool part = int(blockIdx.x) >= a.dw_full;
+    const int j = int(blockIdx.x) - a.dw_full;
+    const int vb = part ? a.dw_full + j / a.tsplit : int(blockIdx.x);
+    const int ts = part ? j % a.tsplit : 0, nts = part ? a.tsplit : 1;
+    const int v0 = vb * 64;
+    const int ntt = (nv + 15) / 16;
+    const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
+    bf16x8_t wf[4][KS];  // B operand of S: W[v0 + 16b + c][q·HS + 32ks + 8g .. +7]
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int v = v0 + 16 * b + c;
+        const uint16_t* wp = a.w + int64_t(v < a.V ? v : 0) * a.ldw + q * HS + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            wf[b][ks] = v < a.V ? *reinterpret_cast<const bf16x8_t*>(wp + 32 * ks) : bf16x8_t{};
+    }
+    f32x16_t acc2[2][CB];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) acc2[b][cb] = f32x16_t{};
+    HsFwdState fs{};
+    hs_engine<G, kHsDw, false>(a, smem, wf, acc2, t0, t1, q, v0, nv, fs);
+    // acc2[b][cb][r] = dW[v0 + 32b + (l&31)][q·HS + 32cb + 8(r>>2) + 4(l>>5) + (r&3)]
+    const int hi = lane >> 5;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int vr = 32 * b + (lane & 31), v = v0 + vr;
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int col = q * HS + 32 * cb + 8 * r4 + 4 * hi;
+                const f32x4_t d = {acc2[b][cb][4 * r4], acc2[b][cb][4 * r4 + 1], acc2[b][cb][4 * r4 + 2],
+                                   acc2[b][cb][4 * r4 + 3]};
+                if (part) {  // fp32 partial of this token split (k_lmloss_dw_reduce)
+                    *reinterpret_cast<f32x4_t*>(a.dwpart + (int64_t(j) * 64 + vr) * a.H + col) = d;
+                } else if (v < a.V) {
+                    const int64_t o = int64_t(v) * a.lddw + col;
+                    if (a.dw_dtype == TRLX_F32)
+                        *reinterpret_cast<f32x4_t*>(static_cast<float*>(a.dw) + o) = d;
+                    else
+                        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.dw) + o) =
+                            make_uint2(pack_bf2(d.x, d.y), pack_bf2(d.z, d.w));
+                }
+            }
+    }
+}
+
+// Forward, H-sliced: per (64-token block, vocab split) the engine over the split's 16-row W
+// tiles; Oᵀ: lane l holds token m0 + 32b + (l&31) at 16 columns in runs of 4; the owner of
+// token block q (16 tokens) holds their (max, Σ) state.
+template <class G, bool RESTART>
+__device__ __forceinline__ void hs_fwd_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit, int nv) {
+    constexpr int KS = G::KS, CB = G::CB, HS = G::HS;
+    const int lane = threadIdx.x & 63;
+    const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, c = lane & 15;
+    const int split = lin / ntb, mt = lin - split * ntb;
+    const int m0 = mt * kLLTokBlock;
+    bf16x8_t hf[4][KS];  // B operand of S: h[token m0 + 16b + c][q·HS + 32ks + 8g .. +7]
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int tm = m0 + 16 * b + c, tc = tm < nv ? tm : nv - 1;
+        const int row = a.rows ? a.rows[tc] : tc;
+        const uint16_t* hp = a.h + int64_t(row) * a.ldh + q * HS + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) hf[b][ks] = *reinterpret_cast<const bf16x8_t*>(hp + 32 * ks);
+    }
+    const int nvt = (a.V + 15) / 16;
+    const int t0 = int(int64_t(split) * nvt / nsplit), t1 = int(int64_t(split + 1) * nvt / nsplit);
+    const int town = m0 + 16 * q + c;  // the token whose softmax state this lane carries
+    const bool vown = town < nv;
+    HsFwdState fs;
+    fs.mfix = -INFINITY;
+    fs.mtrue = -INFINITY;
+    fs.lrun = 0.0f;
+    fs.bad = false;
+    if (RESTART) fs.mfix = a.mlpart[int64_t(split) * a.N + (vown ? town : nv - 1)].x;
+    f32x16_t acc2[2][CB];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) acc2[b][cb] = f32x16_t{};
+    hs_engine<G, kHsFwd, RESTART>(a, smem, hf, acc2, t0, t1, q, 0, nv, fs);
+    bool any = false;
+    if (!RESTART) {
+        any = __any(fs.bad);
+        if (lane == 0) a.flags[lin * 4 + q] = any;
+    }
+    const float mrun = any ? fs.mtrue : fs.mfix;
+    float lt = fs.lrun + __shfl_xor(fs.lrun, 16);
+    lt = lt + __shfl_xor(lt, 32);
+    if (vown && g == 0) a.mlpart[int64_t(split) * a.N + town] = make_float2(mrun, lt);
+    const int hi = lane >> 5;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int tm = m0 + 32 * b + (lane & 31);
+        if (tm < nv) {
+            float* op = a.opart + (int64_t(split) * a.N + tm) * a.H + q * HS + 4 * hi;
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4)
+                    *reinterpret_cast<f32x4_t*>(op + 32 * cb + 8 * r4) =
+                        f32x4_t{acc2[b][cb][4 * r4], acc2[b][cb][4 * r4 + 1], acc2[b][cb][4 * r4 + 2],
+                                acc2[b][cb][4 * r4 + 3]};
+        }
+    }
+}
+
+template <class G, bool RESTART>
+__global__ __launch_bounds__(256, 1) void k_lmloss_fwd_hs(LmLossArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[G::kLds];
+    const int nv = a.rows ? *a.nrows : a.N;
+    const int ntb = (nv + kLLTokBlock - 1) / kLLTokBlock;
+    const int nsplit = ll_fwd_splits(a, ntb);
+    const int total = ntb * nsplit;
+    if (!RESTART) {
+        const int per_xcd = (total + 7) / 8;
+        const int kx = int(blockIdx.x) >> 3, lin = (int(blockIdx.x) & 7) * per_xcd + kx;
+        if (kx >= per_xcd || lin >= total) return;
+        hs_fwd_block<G, false>(a, smem, lin, ntb, nsplit, nv);
+        return;
+    }
+    for (int lin = int(blockIdx.x); lin < total; lin += int(gridDim.x)) {
+        int f = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) f |= a.flags[lin * 4 + w];
+        if (!f) continue;
+        hs_fwd_block<G, true>(a, smem, lin, ntb, nsplit, nv);
+        ll_lds_barrier();
+    }
+}
+
+// ------------------------------------------------------------------ H-sliced, two waves per SIMD
+// The same engine with 8 waves (512 threads, <= 256 registers each): wave w = (group grp =
+// w >> 2, slice q = w & 3) owns register rows 32·grp .. +31 over hidden slice q — 48 operand and
+// 96 accumulator registers at H = 768 — so each SIMD holds one wave of each group, and one
+// wave's stalls (LDS-DMA issue, X-step vector work, LDS waits) sit beside its partner's MFMAs
+// (MI355X_MICROARCH.md 'Two waves per SIMD').  Per tile and wave: S 2 blocks x KS k-steps of
+// 16x16x32, the group's partials summed by owner q (register rows 8q .. 8q+7 of the group, all
+// 16 tile rows: 2 values a lane), P CB blocks of 32x32x16.  LDS as the 4-wave engine (the
+// partial buffers: [group][writer][block][lane] f32x4, 16 KB).
+template <int H_>
+struct Hs8G {
+    static constexpr int H = H_, HS = H / 4, KS = HS / 32, CB = HS / 32;
+    static constexpr int kRows = 16, kTile = kRows * H * 2;
+    static constexpr int kPieces = kTile / 1024, NI = kPieces / 8, NPR = H / 64;
+    static constexpr int kRowGroup = 8 * H * 2;
+    static constexpr int kRing = 5;            // tile slots: 2 tiles of DMA in flight
+    static constexpr int kSlot = kTile + 256;  // + 16 token records (dW)
+    static constexpr int kXBuf = 16 * 1024;
+    static constexpr int kXs = 64 * 32;
+    static constexpr int kLds = kRing * kSlot + 2 * kXBuf + 2 * kXs;
+    static_assert(kPieces % 8 == 0 && kLds <= 163840, "8-wave H-sliced geometry");
+};
+
+template <class G, int ROLE, bool RESTART>
+__device__ __forceinline__ void hs8_engine(const LmLossArgs& a, char* smem, const bf16x8_t (&rop)[2][G::KS],
+                                           f32x16_t (&acc2)[G::CB], int t0, int t1, int w, int v0, int nv,
+                                           HsFwdState& fs) {
+    constexpr int KS = G::KS, CB = G::CB, NI = G::NI;
+    const int lane = threadIdx.x & 63;
+    const int grp = w >> 2, q = w & 3;
+    const int u0 = q * (G::HS / 32);
+    char* slots = smem;
+    char* xbuf = smem + G::kRing * G::kSlot;
+    char* xsb = xbuf + 2 * G::kXBuf;
+    const int rb = hs_rb<G>(lane), trb0 = hs_trb<G>(lane, 0), trb1 = hs_trb<G>(lane, 1);
+    const int xsr = (32 * grp + (lane & 31)) * 32 + 16 * ((lane >> 5) ^ (((lane & 31) >> 3) & 1));
+    // the owner view: register row R8 = 8q + (lane & 7) of the group (block ob = q >> 1, column
+    // oc = 8(q&1) + (lane&7) of its 16x16 partials), tile rows 2j, 2j+1 with j = lane >> 3
+    const int j8 = lane >> 3, oc = 8 * (q & 1) + (lane & 7), ob = q >> 1;
+    const int xoff = ob * 1024 + ((j8 >> 1) * 16 + oc) * 16 + 8 * (j8 & 1);  // in a writer's 2 KB
+    const int xrow = 32 * grp + 16 * ob + oc;                               // X image row
+    const int xsw = xrow * 32 + 16 * ((j8 >> 2) ^ ((xrow >> 3) & 1)) + 4 * (j8 & 3);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        ROLE == kHsDw ? make_rsrc(a.h, uint32_t(int64_t(a.N) * a.ldh * 2)) : make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
+    const int ld2 = ROLE == kHsDw ? int(a.ldh) * 2 : int(a.ldw) * 2;
+    const __amdgpu_buffer_rsrc_t rrec = make_rsrc(a.trec, uint32_t(a.N) * 16u);
+    const __amdgpu_buffer_rsrc_t rrows = make_rsrc(a.rows, a.rows ? uint32_t(a.N) * 4u : 0u);
+    const int rA = (lane >> 2) & 7;
+    auto tok_row = [&](int m) __attribute__((always_inline)) { return m < nv ? (a.rows ? a.rows[m] : m) : a.N; };
+    int nrowA = 0, nrowB = 0;
+    auto piece = [&](int t, char* slot, int k, int rowa, int rowb) __attribute__((always_inline)) {
+        const int i = w + 8 * k;
+        const int r = hs_piece_row<G>(i, lane);
+        int rbytes;
+        if (ROLE == kHsDw)
+            rbytes = int(__umul24(uint32_t(r < 8 ? rowa : rowb), uint32_t(ld2)));
+        else
+            rbytes = (t * 16 + r) * ld2;
+        const int off = rbytes + 16 * hs_piece_chunk<G>(i, lane);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
+                                                 t < t1 ? off : int(0x7ffff000), 0, 0, 0);
+    };
+    auto records = [&](int t, char* slot) __attribute__((always_inline)) {  // lanes 0..15: 256 B
+        const int m = t * 16 + lane;
+        if (lane < 16)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rrec, (__attribute__((address_space(3))) void*)(slot + G::kTile),
+                                                     16, t < t1 && m < nv ? m * 16 : int(0x7ffffff0), 0, 0, 0);
+    };
+    // DMA ops a wave issues per tile (its pieces + wave 0's records): the phase-start wait leaves
+    // the younger tile's in flight
+    const bool recw = ROLE == kHsDw && w == 0;
+    auto slot_of = [&](int t) __attribute__((always_inline)) { return slots + ((t + 2 * G::kRing) % G::kRing) * G::kSlot; };
+    f32x4_t acc[2];
+#if LL_STAMP
+    unsigned long long hst[4] = {};
+    unsigned long long hts0 = 0, hts1 = 0;
+#endif
+    auto body = [&](auto fl_tag, int t, const char* __restrict__ cur, const char* __restrict__ old,
+                    const char* __restrict__ prv, char* __restrict__ nxt, char* __restrict__ xw,
+                    const char* __restrict__ xr, char* __restrict__ xsw_p, const char* __restrict__ xsr_p)
+                    __attribute__((always_inline)) {
+        constexpr int FL = decltype(fl_tag)::value;
+        constexpr bool DS = FL & 1, DX = FL & 2, DP = FL & 4;
+        constexpr int NGS = DS ? 2 * KS : 0, NGP = DP ? CB : 0, NG = NGS + NGP;
+        int pa = 0, pb = 0;  // dW: tile t+2's source rows; the index loads fetch tile t+3's
+        if (ROLE == kHsDw && DS) {
+            const int ma = (t + 2) * 16 + rA, mb = ma + 8;
+            pa = ma < nv ? (a.rows ? nrowA : ma) : a.N;
+            pb = mb < nv ? (a.rows ? nrowB : mb) : a.N;
+            nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * 16 + rA, nv - 1) * 4, 0, 0);
+            nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * 16 + 8 + rA, nv - 1) * 4, 0, 0);
+        }
+        constexpr int PF = 2;
+        bf16x8_t rf[KS];
+        if (DS) {
+#pragma unroll
+            for (int ks = 0; ks < PF && ks < KS; ++ks) rf[ks] = hs_row(cur, rb, u0 + ks);
+            acc[0] = f32x4_t{};
+            acc[1] = f32x4_t{};
+        }
+        bf16x8_t xsf;
+        if (DP) xsf = *reinterpret_cast<const bf16x8_t*>(xsr_p + xsr);
+        float2 xv[4];
+        f32x4_t rec[2];
+        if (DX) {
+#pragma unroll
+            for (int wq = 0; wq < 4; ++wq)
+                xv[wq] = *reinterpret_cast<const float2*>(xr + ((grp * 4 + wq) * 2) * 1024 + xoff);
+            if (ROLE == kHsDw) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r) rec[r] = *reinterpret_cast<const f32x4_t*>(prv + G::kTile + 16 * (2 * j8 + r));
+            }
+        }
+        bf16x8_t tf[CB];
+        float s[2], xo[2];
+        auto xmicro = [&](int m) __attribute__((always_inline)) {
+            if (kLLAblate & 1) return;
+            const int tp = t - 1;
+            if (m == 0) {
+                s[0] = ((xv[0].x + xv[1].x) + xv[2].x) + xv[3].x;
+                s[1] = ((xv[0].y + xv[1].y) + xv[2].y) + xv[3].y;
+                return;
+            }
+            if (ROLE == kHsDw) {
+                if (m == 1) {
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        asm volatile("" ::"v"(rec[r]));
+                        xo[r] = exp2_fast(fmaf(s[r], kLog2e, rec[r].x));
+                    }
+                } else if (m == 2) {
+                    const int vcol = v0 + xrow;
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const float gv = rec[r].y;
+                        xo[r] = fmaf(-gv, xo[r], __float_as_int(rec[r].z) == vcol ? gv : 0.0f);
+                    }
+                } else if (m == 3) {
+                    *reinterpret_cast<uint32_t*>(xsw_p + xsw) = pack_bf2(xo[0], xo[1]);
+                }
+            } else {
+                if (m == 1) {
+                    if ((tp + 1) * 16 > a.V) {  // the vocab's last tile (wave-uniform): rows past V
+                        const int lim = a.V - tp * 16 - 2 * j8;
+                        s[0] = 0 < lim ? s[0] : -INFINITY;
+                        s[1] = 1 < lim ? s[1] : -INFINITY;
+                    }
+                    xo[0] = fmaxf(s[0], s[1]);
+                    // lanes l, l^8 (DPP row_ror:8 within a 16-lane row)
+                    xo[0] = fmaxf(xo[0], __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                             0, __builtin_bit_cast(int, xo[0]), 0x128, 0xf, 0xf, false)));
+                } else if (m == 2) {
+                    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(xo[0]), __float_as_uint(xo[0]),
+                                                                     false, false);
+                    xo[0] = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));  // l, l^16
+                    const float mx = ll_pair_max(xo[0]);                           // l, l^32
+                    if (!RESTART) {
+                        fs.mtrue = fmaxf(fs.mtrue, mx);
+                        fs.mfix = tp == t0 ? mx : fs.mfix;
+                        fs.bad = fs.bad || mx > fs.mfix + kLLOverflow;
+                    }
+                    xo[1] = -fs.mfix * kLog2e;
+                } else if (m == 3) {
+                    s[0] = exp2_fast(fmaf(s[0], kLog2e, xo[1]));
+                    s[1] = exp2_fast(fmaf(s[1], kLog2e, xo[1]));
+                    fs.lrun += s[0] + s[1];
+                    *reinterpret_cast<uint32_t*>(xsw_p + xsw) = pack_bf2(s[0], s[1]);
+                }
+            }
+        };
+        constexpr int NXM = 4;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            if (k < NGS) {
+                const int ks = k >> 1, b = k & 1;
+                if (b == 0 && ks + PF < KS) rf[ks + PF] = hs_row(cur, rb, u0 + ks + PF);
+                acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rf[ks], rop[b][ks], acc[b], 0, 0, 0);
+                if ((k & 3) == 1 && (k >> 2) < NI && !(kLLAblate & 4) && t + 2 < t1) {
+                    piece(t + 2, nxt, k >> 2, pa, pb);
+                    if (recw && (k >> 2) == 0) records(t + 2, nxt);
+                }
+                if (DP && k == NGS - 4) tf[0] = hs_tr(old, trb0, trb1, u0);
+                if (DP && k == NGS - 2 && CB > 1) tf[1] = hs_tr(old, trb0, trb1, u0 + 1);
+            } else if (k < NG) {
+                const int cb = k - NGS;
+                if (!DS && cb == 0) {
+                    tf[0] = hs_tr(old, trb0, trb1, u0);
+                    if (CB > 1) tf[1] = hs_tr(old, trb0, trb1, u0 + 1);
+                }
+                if (cb + 2 < CB) tf[cb + 2] = hs_tr(old, trb0, trb1, u0 + cb + 2);
+                acc2[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[cb], xsf, acc2[cb], 0, 0, 0);
+                if (DS && (cb == 1 || cb == 2))  // S(t)'s partials: [group][writer][block]
+                    reinterpret_cast<f32x4_t*>(xw + ((grp * 4 + q) * 2 + cb - 1) * 1024)[lane] = acc[cb - 1];
+            }
+            if (DX) {
+                constexpr int XK0 = DP ? NGS + 1 : (NGS >= NXM ? NGS - NXM : 0);
+#pragma unroll
+                for (int m = 0; m < NXM; ++m)
+                    if (k == XK0 + m) xmicro(m);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#if LL_STAMP
+            if (FL == 7 && k == NGS - 1) {
+                unsigned long long tsx = 0;
+                LL_TS(tsx);
+                hst[1] += tsx - hts1;
+                hts1 = tsx;
+            }
+#endif
+        }
+        if (DS && (!DP || CB < 3)) {  // no P MFMAs (or too few) to carry them: S(t)'s partials now
+#pragma unroll
+            for (int b = (DP ? CB - 1 : 0); b < 2; ++b)
+                reinterpret_cast<f32x4_t*>(xw + ((grp * 4 + q) * 2 + b) * 1024)[lane] = acc[b];
+        }
+        if (DX) {  // micro-steps the gaps did not hold
+            constexpr int XK0 = DP ? NGS + 1 : (NGS >= NXM ? NGS - NXM : 0);
+#pragma unroll
+            for (int m = 0; m < NXM; ++m)
+                if (XK0 + m >= NG) xmicro(m);
+        }
+#if LL_STAMP
+        if (FL == 7) {
+            unsigned long long tsx = 0;
+            LL_TS(tsx);
+            hst[2] += tsx - hts1;
+            hst[3] += 1;
+        }
+#endif
+    };
+    auto phase = [&](auto fl_tag, int t) __attribute__((always_inline)) {
+#if LL_STAMP
+        LL_TS(hts0);
+#endif
+        // tile t landed (this wave's pieces; the barrier: everyone's); the younger tile's pieces
+        // (issued by the previous phase) stay in flight
+        // (past the split no tile is fetched at all: a load whose every lane is out of range is
+        // not counted in order with the others — measured: the counted wait then let a real
+        // tile's reads run ahead of its data)
+        if (decltype(fl_tag)::value == 4 || t + 1 >= t1)
+            __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));
+        else if (recw)
+            __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI + 1));
+        else
+            __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI));
+        ll_lds_barrier();
+#if LL_STAMP
+        LL_TS(hts1);
+        if (decltype(fl_tag)::value == 7) hst[0] += hts1 - hts0;
+#endif
+        body(fl_tag, t, slot_of(t), slot_of(t - 2), slot_of(t - 1), slot_of(t + 2), xbuf + (t & 1) * G::kXBuf,
+             xbuf + ((t - 1) & 1) * G::kXBuf, xsb + ((t - 1) & 1) * G::kXs, xsb + ((t - 2) & 1) * G::kXs);
+    };
+    if (t0 >= t1) return;
+    // the register operand has landed before the first tile's DMA: the phase waits count DMA ops
+    // only (a load the compiler sank below the prologue's pieces would be the youngest op)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(rop[b][ks]));
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {  // prologue: tiles t0 and t0+1
+        if (t0 + tt >= t1) break;
+        char* s0 = slot_of(t0 + tt);
+        const int m = (t0 + tt) * 16 + rA;
+        const int ra0 = ROLE == kHsDw ? tok_row(m) : 0, rb0 = ROLE == kHsDw ? tok_row(m + 8) : 0;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) piece(t0 + tt, s0, k, ra0, rb0);
+        if (recw) records(t0 + tt, s0);
+    }
+    if (ROLE == kHsDw && a.rows) {  // tile t0+2's row indices
+        nrowA = a.rows[min((t0 + 2) * 16 + rA, nv - 1)];
+        nrowB = a.rows[min((t0 + 2) * 16 + 8 + rA, nv - 1)];
+    }
+    using F1 = std::integral_constant<int, 1>;
+    using F3 = std::integral_constant<int, 3>;
+    using F7 = std::integral_constant<int, 7>;
+    using F6 = std::integral_constant<int, 6>;
+    using F2 = std::integral_constant<int, 2>;
+    using F4 = std::integral_constant<int, 4>;
+    phase(F1{}, t0);
+    if (t0 + 1 < t1) {
+        phase(F3{}, t0 + 1);
+        for (int t = t0 + 2; t < t1; ++t) phase(F7{}, t);
+        phase(F6{}, t1);
+    } else {
+        phase(F2{}, t1);
+    }
+    phase(F4{}, t1 + 1);
+#if LL_STAMP
+    {
+        const int slot = int(blockIdx.x) * 8 + w;
+        if (lane == 0 && slot < (1 << 12))
+            for (int k = 0; k < 4; ++k) g_ll_stamps[(ROLE == kHsDw ? (1 << 15) : 0) + slot * 8 + k] = hst[k];
+    }
+#endif
+}
+
+template <class G>
+__global__ __launch_bounds__(512, 2) void k_lmloss_dw_hs8(LmLossArgs a) {
+    constexpr int KS = G::KS, CB = G::CB, HS = G::HS;
+    __shared__ __attribute__((aligned(16))) char smem[G::kLds];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = w >> 2, q = w & 3;
+    const int g = lane >> 4, c = lane & 15;
+    const int nv = a.rows ? *a.nrows : a.N;
+    const bool part = int(blockIdx.x) >= a.dw_full;
+    const int j = int(blockIdx.x) - a.dw_full;
+    const int vb = part ? a.dw_full + j / a.tsplit : int(blockIdx.x);
+    const int ts = part ? j % a.tsplit : 0, nts = part ? a.tsplit : 1;
+    const int v0 = vb * 64;
+    const int ntt = (nv + 15) / 16;
+    const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
+    bf16x8_t wf[2][KS];  // B operand of S: W[v0 + 32grp + 16b + c][q·HS + 32ks + 8g .. +7]
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int v = v0 + 32 * grp + 16 * b + c;
+        const uint16_t* wp = a.w + int64_t(v < a.V ? v : 0) * a.ldw + q * HS + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            wf[b][ks] = v < a.V ? *reinterpret_cast<const bf16x8_t*>(wp + 32 * ks) : bf16x8_t{};
+    }
+    f32x16_t acc2[CB];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) acc2[cb] = f32x16_t{};
+    HsFwdState fs{};
+    hs8_engine<G, kHsDw, false>(a, smem, wf, acc2, t0, t1, w, v0, nv, fs);
+    const int hi = lane >> 5;
+    const int vr = 32 * grp + (lane & 31), v = v0 + vr;
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+            const int col = q * HS + 32 * cb + 8 * r4 + 4 * hi;
+            const f32x4_t d = {acc2[cb][4 * r4], acc2[cb][4 * r4 + 1], acc2[cb][4 * r4 + 2], acc2[cb][4 * r4 + 3]};
+            if (part) {
+                *reinterpret_cast<f32x4_t*>(a.dwpart + (int64_t(j) * 64 + vr) * a.H + col) = d;
+            } else if (v < a.V) {
+                const int64_t o = int64_t(v) * a.lddw + col;
+                if (a.dw_dtype == TRLX_F32)
+                    *reinterpret_cast<f32x4_t*>(static_cast<float*>(a.dw) + o) = d;
+                else
+                    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.dw) + o) =
+                        make_uint2(pack_bf2(d.x, d.y), pack_bf2(d.z, d.w));
+            }
+        }
+}
+
+template <class G, bool RESTART>
+__device__ __forceinline__ void hs8_fwd_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit, int nv) {
+    constexpr int KS = G::KS, CB = G::CB, HS = G::HS;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int grp = w >> 2, q = w & 3;
+    const int g = lane >> 4, c = lane & 15;
+    const int split = lin / ntb, mt = lin - split * ntb;
+    const int m0 = mt * kLLTokBlock;
+    bf16x8_t hf[2][KS];  // B operand of S: h[token m0 + 32grp + 16b + c][q·HS + 32ks + 8g .. +7]
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int tm = m0 + 32 * grp + 16 * b + c, tc = tm < nv ? tm : nv - 1;
+        const int row = a.rows ? a.rows[tc] : tc;
+        const uint16_t* hp = a.h + int64_t(row) * a.ldh + q * HS + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) hf[b][ks] = *reinterpret_cast<const bf16x8_t*>(hp + 32 * ks);
+    }
+    const int nvt = (a.V + 15) / 16;
+    const int t0 = int(int64_t(split) * nvt / nsplit), t1 = int(int64_t(split + 1) * nvt / nsplit);
+    // the token whose softmax state this lane carries (owner view: 8q + (lane&7) of the group)
+    const int town = m0 + 32 * grp + 8 * q + (lane & 7);
+    const bool vown = town < nv;
+    HsFwdState fs;
+    fs.mfix = -INFINITY;
+    fs.mtrue = -INFINITY;
+    fs.lrun = 0.0f;
+    fs.bad = false;
+    if (RESTART) fs.mfix = a.mlpart[int64_t(split) * a.N + (vown ? town : nv - 1)].x;
+    f32x16_t acc2[CB];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) acc2[cb] = f32x16_t{};
+    hs8_engine<G, kHsFwd, RESTART>(a, smem, hf, acc2, t0, t1, w, 0, nv, fs);
+    bool any = false;
+    if (!RESTART) {
+        any = __any(fs.bad);
+        if (lane == 0) a.flags[lin * 8 + w] = any;
+    }
+    const float mrun = any ? fs.mtrue : fs.mfix;
+    // the token's Σ over its 8 lanes (l ^ 8, l ^ 16, l ^ 32)
+    float lt = fs.lrun + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, fs.lrun),
+                                                                                0x128, 0xf, 0xf, false));
+    {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(lt), __float_as_uint(lt), false, false);
+        lt = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    lt = ll_pair_sum(lt);
+    if (vown && lane < 8) a.mlpart[int64_t(split) * a.N + town] = make_float2(mrun, lt);
+    const int hi = lane >> 5;
+    const int tm = m0 + 32 * grp + (lane & 31);
+    if (tm < nv) {
+        float* op = a.opart + (int64_t(split) * a.N + tm) * a.H + q * HS + 4 * hi;
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4)
+                *reinterpret_cast<f32x4_t*>(op + 32 * cb + 8 * r4) =
+                    f32x4_t{acc2[cb][4 * r4], acc2[cb][4 * r4 + 1], acc2[cb][4 * r4 + 2], acc2[cb][4 * r4 + 3]};
+    }
+}
+
+template <class G, bool RESTART>
+__global__ __launch_bounds__(512, 2) void k_lmloss_fwd_hs8(LmLossArgs a) {
+    __shared__ __attribute__((aligned(16))) char smem[G::kLds];
+    const int nv = a.rows ? *a.nrows : a.N;
+    const int ntb = (nv + kLLTokBlock - 1) / kLLTokBlock;
+    const int nsplit = ll_fwd_splits(a, ntb);
+    const int total = ntb * nsplit;
+    if (!RESTART) {
+        const int per_xcd = (total + 7) / 8;
+        const int kx = int(blockIdx.x) >> 3, lin = (int(blockIdx.x) & 7) * per_xcd + kx;
+        if (kx >= per_xcd || lin >= total) return;
+        hs8_fwd_block<G, false>(a, smem, lin, ntb, nsplit, nv);
+        return;
+    }
+    for (int lin = int(blockIdx.x); lin < total; lin += int(gridDim.x)) {
+        int f = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) f |= a.flags[lin * 8 + w];
+        if (!f) continue;
+        hs8_fwd_block<G, true>(a, smem, lin, ntb, nsplit, nv);
+        ll_lds_barrier();
+    }
+}
+
 // ------------------------------------------------------------------ host side
 static TuneKnob g_ll_splits{0};  // tuning "lmloss_splits" (0 = auto)
 static TuneKnob g_ll_tsplit{0};  // tuning "lmloss_dw_tsplit" (0 = auto)
 // tuning "lmloss_fwd": 0 auto (= 1), 1 the 32x32x16 pair form (ll_fwd_block), 2 the 16x16x32 form
 // (ll_fwd16_block: no exchange, but twice the LDS bytes per MFMA — measured 1123 vs ~1010 us
-// at C2, while the same trade won for dW, whose exchange and dS sat on the critical path)
+// at C2, while the same trade won for dW, whose exchange and dS sat on the critical path),
+// 3 the H-sliced form (k_lmloss_fwd_hs)
 static TuneKnob g_ll_fwd{0};
+// tuning "lmloss_dw": 0 auto (= 1), 1 the row-split 16x16x32 form (k_lmloss_dw), 2 the H-sliced
+// form (k_lmloss_dw_hs)
+static TuneKnob g_ll_dw{0};
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
     const bool sp = key && !__builtin_strcmp(key, "lmloss_splits");
     const bool ts = key && !__builtin_strcmp(key, "lmloss_dw_tsplit");
     const bool fw = key && !__builtin_strcmp(key, "lmloss_fwd");
-    *handled = sp || ts || fw;
+    const bool dwk = key && !__builtin_strcmp(key, "lmloss_dw");
+    *handled = sp || ts || fw || dwk;
     if (fw) {
-        TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "lmloss_fwd: 0 auto (1), 1 32x32 pair form, 2 16x16 form");
+        TRLX_REQUIRE(value >= 0 && value <= 4, TRLX_ERR_ARG,
+                     "lmloss_fwd: 0 auto, 1 32x32 pair form, 2 16x16 form, 3 H-sliced form, 4 H-sliced 8-wave form");
         g_ll_fwd = int(value);
+        return TRLX_OK;
+    }
+    if (dwk) {
+        TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG,
+                     "lmloss_dw: 0 auto, 1 row-split form, 2 H-sliced form, 3 H-sliced 8-wave form");
+        g_ll_dw = int(value);
         return TRLX_OK;
     }
     if (sp) {
@@ -1355,7 +2321,7 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, boo
     t.trec = reinterpret_cast<float*>(take(size_t(N) * 16));
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t(order_chunks(N) + 1) * 4));
-    t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 4 * 4));  // <= 4 waves per workgroup
+    t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 8 * 4));  // <= 8 waves per workgroup
     const LlDwPlan dp = ll_dw_plan(V);
     t.dwpart = reinterpret_cast<float*>(take(size_t(dp.nblk) * dp.tsplit * kLLTokBlock * H * 4));
     if (w) *w = t;
@@ -1384,10 +2350,26 @@ static int ll_check(const void* hidden, int64_t ldh, const void* weight, int64_t
 
 // The forward's grid covers the largest split plan (every token live, a.nsplit splits),
 // rounded up to whole XCD shares; each workgroup finds its (token block, split) on the device.
-template <class G>
+template <class G, class HG, class H8>
 static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
     const int64_t ntb = (a.N + kLLTokBlock - 1) / kLLTokBlock;
     const unsigned grid = unsigned((ntb * a.nsplit + 7) / 8 * 8);
+    if (g_ll_fwd == 4) {
+        hipLaunchKernelGGL((k_lmloss_fwd_hs8<H8, false>), dim3(grid), dim3(512), 0, s, a);
+        const int rc = check_launch("k_lmloss_fwd_hs8");
+        if (rc) return rc;
+        hipLaunchKernelGGL((k_lmloss_fwd_hs8<H8, true>), dim3(unsigned(std::min<int64_t>(grid, a.ncu))), dim3(512), 0,
+                           s, a);
+        return check_launch("k_lmloss_fwd_hs8 restart");
+    }
+    if (g_ll_fwd == 3) {
+        hipLaunchKernelGGL((k_lmloss_fwd_hs<HG, false>), dim3(grid), dim3(256), 0, s, a);
+        const int rc = check_launch("k_lmloss_fwd_hs");
+        if (rc) return rc;
+        hipLaunchKernelGGL((k_lmloss_fwd_hs<HG, true>), dim3(unsigned(std::min<int64_t>(grid, a.ncu))), dim3(256), 0,
+                           s, a);
+        return check_launch("k_lmloss_fwd_hs restart");
+    }
     const bool f16 = g_ll_fwd == 2;
     void (*first)(LmLossArgs) = f16 ? k_lmloss_fwd<G, false, true> : k_lmloss_fwd<G, false, false>;
     void (*restart)(LmLossArgs) = f16 ? k_lmloss_fwd<G, true, true> : k_lmloss_fwd<G, true, false>;
@@ -1397,16 +2379,25 @@ static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(restart, dim3(unsigned(std::min<int64_t>(grid, a.ncu))), dim3(G::kThreads), 0, s, a);
     return check_launch("k_lmloss_fwd restart");
 }
-template <class G>
+template <class G, class HG, class H8>
 static int ll_launch_dw(const LmLossArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lmloss_dw<G>, dim3(unsigned(a.dw_full + a.dw_nblk * a.tsplit)), dim3(G::kThreads), 0, s, a);
+    const dim3 grid(unsigned(a.dw_full + a.dw_nblk * a.tsplit));
+    if (g_ll_dw == 3) {
+        hipLaunchKernelGGL(k_lmloss_dw_hs8<H8>, grid, dim3(512), 0, s, a);
+        return check_launch("k_lmloss_dw_hs8");
+    }
+    if (g_ll_dw == 2) {
+        hipLaunchKernelGGL(k_lmloss_dw_hs<HG>, grid, dim3(256), 0, s, a);
+        return check_launch("k_lmloss_dw_hs");
+    }
+    hipLaunchKernelGGL(k_lmloss_dw<G>, grid, dim3(G::kThreads), 0, s, a);
     return check_launch("k_lmloss_dw");
 }
 static int ll_fwd(const LmLossArgs& a, hipStream_t s) {
-    return a.H == 512 ? ll_launch_fwd<LlG512>(a, s) : ll_launch_fwd<LlG768>(a, s);
+    return a.H == 512 ? ll_launch_fwd<LlG512, HsG<512>, Hs8G<512>>(a, s) : ll_launch_fwd<LlG768, HsG<768>, Hs8G<768>>(a, s);
 }
 static int ll_dw(const LmLossArgs& a, hipStream_t s) {
-    return a.H == 512 ? ll_launch_dw<LlG512>(a, s) : ll_launch_dw<LlG768>(a, s);
+    return a.H == 512 ? ll_launch_dw<LlG512, HsG<512>, Hs8G<512>>(a, s) : ll_launch_dw<LlG768, HsG<768>, Hs8G<768>>(a, s);
 }
 
 // the common part: shapes, workspace, optional compaction from the mask
@@ -1439,6 +2430,9 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.mlpart = w.mlpart;
     a.trec = w.trec;
     a.flags = w.flags;
+    // dW rows are stored in runs of 4 columns (16 B fp32, 8 B bf16)
+    TRLX_REQUIRE(!dweight || (lddw % 4 == 0 && (reinterpret_cast<uintptr_t>(dweight) & 15) == 0), TRLX_ERR_STRIDE,
+                 "dweight must be 16-B aligned with a row stride that is a multiple of 4 elements");
     a.dw = dweight;
     a.lddw = lddw;
     a.dw_dtype = dw_dtype;
