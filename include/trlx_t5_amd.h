@@ -355,9 +355,16 @@ int trlx_lmhead_logprobs_ragged(const void* hidden, int64_t ldh, const void* wei
  * [N, lddh] of dh_dtype (bf16 / fp32, lddh a multiple of 4).  Three MFMA launches + small
  * ones: a flash-style forward (online softmax and O = Σ_v P·W_v per token and vocab split), a
  * per-token combine (lse, lp, g, dh) and a dW pass that recomputes each logits tile and
- * accumulates dSᵀ·h; deterministic (fixed-order sums, no atomics).
+ * accumulates dSᵀ·h — or, in the PPO entries given the larger saved-P workspace, reads the
+ * forward's bf16 P tiles back instead of recomputing them; deterministic (fixed-order sums, no
+ * atomics).
  * lm_workspace: trlx_lmhead_loss_workspace_bytes(N, H, V) bytes, no initialisation. */
 int64_t trlx_lmhead_loss_workspace_bytes(int64_t N, int64_t H, int64_t V);
+/* The PPO entries' workspace with room for the saved-P plan (the forward's bf16 P tiles,
+ * ⌈V/64⌉·2⌈N/64⌉·4 KB: 0.62 GB at N = 6144, V = 50257, plus per-(split, token) records).  Pass
+ * its size as lm_workspace_bytes; a workspace of only trlx_lmhead_loss_workspace_bytes runs the
+ * recompute plan. */
+int64_t trlx_ppo_loss_from_hidden_workspace_bytes(int64_t N, int64_t H, int64_t V);
 /* The smaller workspace trlx_lmhead_logprobs_bwd needs (no forward partials). */
 int64_t trlx_lmhead_loss_bwd_workspace_bytes(int64_t N, int64_t H, int64_t V);
 /* The PPO loss from the policy's last hidden states: trlx_ppo_loss_rows's arguments with the
@@ -366,7 +373,9 @@ int64_t trlx_lmhead_loss_bwd_workspace_bytes(int64_t N, int64_t H, int64_t V);
  * `stats` (NULL: adv_raw used as given, and then only mask = NULL: the loss normaliser Σ mask
  * is read at stats[3]), dvalues, lp_out.  Tokens with mask == 0 are skipped (compacted out of
  * all three MFMA passes: zero gradient, lp_out 0, their token records as the masked loss rows
- * write them).  N·ldh·2 and V·ldw·2 must stay below 2 GB (32-bit tile addressing). */
+ * write them).  N·ldh·2 and V·ldw·2 must stay below 2 GB (32-bit tile addressing).
+ * lm_workspace_bytes: the size of lm_workspace (>= trlx_lmhead_loss_workspace_bytes, else
+ * TRLX_ERR_ARG; >= trlx_ppo_loss_from_hidden_workspace_bytes selects the saved-P plan). */
 int trlx_ppo_loss_from_hidden(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t B,
                               int64_t T, int64_t H, int64_t V, const int64_t* labels, const void* old_lp,
                               int old_dtype, const float* adv_raw, const double* stats, int unbiased,
@@ -374,7 +383,7 @@ int trlx_ppo_loss_from_hidden(const void* hidden, int64_t ldh, const void* weigh
                               int ov_dtype, const void* returns, int r_dtype, float cliprange,
                               float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
                               int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues,
-                              void* workspace, void* lm_workspace, void* stream);
+                              void* workspace, void* lm_workspace, int64_t lm_workspace_bytes, void* stream);
 /* The split-beta form (the pipelined data-parallel schedule; see trlx_ppo_loss_rows_split /
  * trlx_ppo_loss_rows_split_gae): the advantage A0 - beta*Ak whitened by coefficients that are
  * either given (`coef`, stored by an earlier loss on the same experience) or derived here from
@@ -391,7 +400,8 @@ int trlx_ppo_loss_from_hidden_split(const void* hidden, int64_t ldh, const void*
                                     int ov_dtype, float* rewards, void* returns, int r_dtype, float cliprange,
                                     float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
                                     int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues,
-                                    void* workspace, void* lm_workspace, void* stream);
+                                    void* workspace, void* lm_workspace, int64_t lm_workspace_bytes,
+                                    void* stream);
 /* The differentiable building block (logprobs_from_logits(lm_head(h), y) with autograd):
  * forward -> lp [N] (lp_dtype), lse [N] fp32 and E = Σ_v p_tv·W_v [N, H] fp32 (saved for the
  * backward); backward(grad = d loss / d lp [N], F32 / BF16) -> dhidden, dweight (either may be

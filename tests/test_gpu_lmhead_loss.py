@@ -402,24 +402,12 @@ def test_lm_head_loss_side_halves(kind, N, H, V, form):
         P._lib.set_tuning("lmloss_fwd", 0)
 
 
-@pytest.mark.parametrize("B,T,V,H,masked,kind", [(128, 48, 50257, 768, False, "flat"),
-                                                 (128, 48, 50257, 768, False, "peaked"),
-                                                 (256, 48, 32128, 768, True, "flat"),
-                                                 (256, 48, 32128, 768, True, "peaked")])
-def test_hot_path_loss_side_halves(B, T, V, H, masked, kind):
-    """PPOHotPath.step_from_hidden (the PPO route, trlx_ppo_loss_from_hidden) at the C2 and C3
-    shards, fp32 gradients, against the oracle's loss side in fp64 (lm_head logits, the
-    oracle's logprobs_from_logits + ppo_loss, autograd): dh per token against the E term it
-    carries, dW on the non-label rows, the label rows and per row (masked tokens contribute
-    nothing and their hidden rows are NaN on the device)."""
-    x = _ppo_inputs(B, T, V, H, 300 + B + T, masked)
-    if kind == "peaked":
-        nh, w, y = C.peaked_operands(B * T, H, V, 301 + B)
-        x["new_h"], x["w"], x["labels"] = nh.view(B, T, H), w, y.view(B, T)
-        x["h"] = (nh.float() + 0.05 * torch.randn(B * T, H, generator=torch.Generator().manual_seed(3))).to(
-            torch.bfloat16).view(B, T, H)
-        x["ref_h"] = (x["h"].float() + 0.1 * torch.randn(B, T, H, generator=torch.Generator().manual_seed(4))).to(
-            torch.bfloat16)
+def _hot_path_halves(x, B, T, V, H, masked, label):
+    """PPOHotPath.step_from_hidden with fp32 gradients against the oracle's loss side in fp64
+    (lm_head logits of the same bf16 operands, logprobs_from_logits + ppo_loss, autograd) on
+    the product's own experience outputs: the loss, dh per token against the E term it
+    carries, dW on the non-label rows, the label rows and per row (lmloss_checks); masked
+    tokens contribute nothing and their hidden rows are NaN on the device."""
     d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in x.items()}
     if masked:
         d["new_h"] = d["new_h"].masked_fill((d["mask"] == 0)[..., None], float("nan"))
@@ -433,7 +421,6 @@ def test_hot_path_loss_side_halves(B, T, V, H, masked, kind):
     st = hp.adv_stats.cpu()
     mu, var = P.modeling.moments_to_mean_var(st, unbiased=True)
     adv_w = ((hp.adv_raw.cpu().double() - mu) * torch.rsqrt(var + 1e-8))
-    # fp64 loss side: the same bf16 operands, the product's own experience outputs
     N = B * T
     hd = x["new_h"].double().to(DEV).reshape(N, H).requires_grad_(True)
     wd = x["w"].double().to(DEV).requires_grad_(True)
@@ -452,8 +439,67 @@ def test_hot_path_loss_side_halves(B, T, V, H, masked, kind):
     errs = C.dw_errors(dw, wd.grad, x["labels"].reshape(-1)[live])
     errs.update(C.dh_errors(dh.reshape(N, H)[live.to(DEV)], hd.grad[live.to(DEV)], g[live.to(DEV)],
                             e64[live.to(DEV)], fp32_out=True))
-    C.assert_within(errs, f"hot path {kind} B={B} V={V} masked={masked}")
+    C.assert_within(errs, label)
     assert (dh.reshape(N, H)[~live.to(DEV)] == 0).all()
+    return [t.clone() for t in (loss, stats, dh, dw, dv)] + [hp.lp_new.clone()]
+
+
+@pytest.mark.parametrize("B,T,V,H,masked,kind", [(128, 48, 50257, 768, False, "flat"),
+                                                 (128, 48, 50257, 768, False, "peaked"),
+                                                 (256, 48, 32128, 768, True, "flat"),
+                                                 (256, 48, 32128, 768, True, "peaked")])
+@pytest.mark.parametrize("plan", [0, 1])
+def test_hot_path_loss_side_halves(B, T, V, H, masked, kind, plan):
+    """PPOHotPath.step_from_hidden (the PPO route, trlx_ppo_loss_from_hidden) at the C2 and C3
+    shards against fp64 (_hot_path_halves), on both dW plans: plan 0 = the default saved-P plan
+    (k_lmloss_dwp reads the forward's bf16 P back: its label entries from the fp32 label logit),
+    plan 1 = Sᵀ recomputed (k_lmloss_dw)."""
+    x = _ppo_inputs(B, T, V, H, 300 + B + T, masked)
+    if kind == "peaked":
+        nh, w, y = C.peaked_operands(B * T, H, V, 301 + B)
+        x["new_h"], x["w"], x["labels"] = nh.view(B, T, H), w, y.view(B, T)
+        x["h"] = (nh.float() + 0.05 * torch.randn(B * T, H, generator=torch.Generator().manual_seed(3))).to(
+            torch.bfloat16).view(B, T, H)
+        x["ref_h"] = (x["h"].float() + 0.1 * torch.randn(B, T, H, generator=torch.Generator().manual_seed(4))).to(
+            torch.bfloat16)
+    P._lib.set_tuning("lmloss_dw", plan)
+    try:
+        _hot_path_halves(x, B, T, V, H, masked, f"hot path plan {plan} {kind} B={B} V={V} masked={masked}")
+    finally:
+        P._lib.set_tuning("lmloss_dw", 0)
+
+
+@pytest.mark.parametrize("splits,tsplit", [(1, 1), (3, 2), (8, 5), (5, 16)])
+def test_hot_path_saved_p_plans(splits, tsplit):
+    """The saved-P plan under forced grid plans (vocab splits: each dW wave rescales its P by
+    its own split's offset; dW token splits: partials + the fixed-order reduce) and with the
+    forward's restart (a logit jump of ~80 from the 3rd W tile on: the restarted blocks rewrite
+    their P tiles and offsets), ragged masked batch and H = 512 and 768: fp64 halves checks, and
+    against the recompute plan on the same step."""
+    for B, T, V, H, jump in ((8, 20, 7000, 768, False), (8, 20, 7000, 768, True), (6, 11, 1031, 512, True)):
+        x = _ppo_inputs(B, T, V, H, 40 + splits + tsplit, True)
+        if jump:
+            wf = x["w"].float()
+            dvec = x["new_h"].float().reshape(-1, H).mean(0)
+            wf[2 * 32:] += 80.0 * dvec / (dvec @ dvec)
+            x["w"] = wf.to(torch.bfloat16)
+        P._lib.set_tuning("lmloss_splits", splits)
+        P._lib.set_tuning("lmloss_dw_tsplit", tsplit)
+        outs = {}
+        try:
+            for plan in (0, 1):
+                P._lib.set_tuning("lmloss_dw", plan)
+                outs[plan] = _hot_path_halves(x, B, T, V, H, True,
+                                              f"saved-P splits={splits} tsplit={tsplit} H={H} jump={jump} plan={plan}")
+        finally:
+            for k in ("lmloss_dw", "lmloss_splits", "lmloss_dw_tsplit"):
+                P._lib.set_tuning(k, 0)
+        a, b = outs[1], outs[0]
+        torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(b[4], a[4], rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(b[5], a[5], rtol=1e-5, atol=1e-5)
+        assert torch.equal(b[2], a[2])  # dh comes from the combine: the plans differ in dW only
+        assert _rel(b[3], a[3]) < 4e-3
 
 
 @pytest.mark.parametrize("kind,N,H,V", [("flat", 6144, 768, 50257), ("peaked", 6144, 768, 50257),
@@ -529,7 +575,7 @@ def test_hot_path_h_sliced_matches_row_split(B, T, V, H, masked):
     if masked:
         d["new_h"] = d["new_h"].masked_fill((d["mask"] == 0)[..., None], float("nan"))
     outs = {}
-    for fwd, dw in ((1, 1), (3, 2), (4, 3)):
+    for fwd, dw in ((1, 1), (3, 2), (4, 3), (0, 0)):
         P._lib.set_tuning("lmloss_fwd", fwd)
         P._lib.set_tuning("lmloss_dw", dw)
         try:
@@ -543,7 +589,7 @@ def test_hot_path_h_sliced_matches_row_split(B, T, V, H, masked):
             P._lib.set_tuning("lmloss_fwd", 0)
             P._lib.set_tuning("lmloss_dw", 0)
     a = outs[1]
-    for f in (3, 4):
+    for f in (3, 4, 0):  # 0: the defaults (16x16 forward, saved-P dW)
         b = outs[f]
         torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(b[1], a[1], rtol=1e-4, atol=1e-6)

@@ -13,7 +13,10 @@ outputs (loss + stats via the loss tail, dvalues, d hidden, d lm_head weight in 
 Interleaved rounds; HIP-event time per call (median), TFLOP/s against the 4·N·V·H·2 flops
 the fused route executes (the unfused route's 3 GEMMs are 3·N·V·H·2).
 
-  python tools/lossside_bench.py [--config c2|c3] [--iters 20] [--rounds 3]
+  python tools/lossside_bench.py [--config c2|c3] [--iters 20] [--rounds 3] [--routes gemm,fused,fused_recompute]
+
+  (fused = the default saved-P plan: the forward stores its bf16 P tiles, the dW pass reads them
+  back; fused_recompute = the dW pass recomputing the logits tiles)
 """
 import argparse
 import json
@@ -78,7 +81,14 @@ def main():
     def fused():
         hp.policy_loss_from_hidden(new_h, w, labels, values, old_values, mask=mask)
 
-    routes = {"gemm": gemm, "fused": fused}
+    def fused_recompute():  # the dW kernel recomputing S^T (k_lmloss_dw) instead of the saved P
+        P._lib.set_tuning("lmloss_dw", 1)
+        try:
+            fused()
+        finally:
+            P._lib.set_tuning("lmloss_dw", 0)
+
+    routes = {"gemm": gemm, "fused": fused, "fused_recompute": fused_recompute}
     names = args.routes.split(",")
     for n in names:  # warm up (and hipBLASLt heuristics)
         for _ in range(3):

@@ -128,13 +128,14 @@ SIGNATURES = {
     "trlx_ppo_loss_from_hidden": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp,
                                            _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp,
                                            _c_int, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_i64, _c_int, _c_vp,
-                                           _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+                                           _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_lmhead_loss_bwd_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64]),
+    "trlx_ppo_loss_from_hidden_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64]),
     "trlx_ppo_loss_from_hidden_split": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
                                                  _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,
                                                  _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp,
                                                  _c_int, _c_f, _c_f, _c_f, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_int,
-                                                 _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+                                                 _c_i64, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_lmhead_logprobs_fwd_saved": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
                                                 _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "trlx_lmhead_logprobs_bwd": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp,

@@ -52,7 +52,9 @@ constexpr float kLLOverflow = 60.0f;
 constexpr int64_t kLLMaxSpan = 0x7fff0000;
 // Diagnostic builds only (-DLL_ABLATE=bits, never the shipped library): drop parts of the
 // forward's steady-state step to price them — 1 softmax, 2 group-sum exchange, 4 next DMA,
-// 8 O product, 16 S product.  Results are wrong in such a build.
+// 8 O product, 16 S product; saved-P stores: 32 no global store, 64 no LDS transpose; the
+// saved-P dW kernel: 128 no P loads, 256 no h DMA, 512 dS kept from the first tile.  Results
+// are wrong in such a build.
 #ifndef LL_ABLATE
 #define LL_ABLATE 0
 #endif
@@ -113,7 +115,13 @@ struct LmLossArgs {
     // blocks are split tsplit ways over the tokens into fp32 partials ([j][vpw][H]) that
     // k_lmloss_dw_reduce sums in split order (the last, partial round of workgroups)
     int dw_full, tsplit, dw_nblk;
+    int dw_vpw;      // vocab rows per dW workgroup (64; the saved-P plan's RW = 2 form: 128)
     float* dwpart;
+    // saved-P plan (k_lmloss_dwp): the forward stores its bf16 P tiles in the dW kernel's layout
+    // (ll_p_save), the combine a per-(split, token) record {g·e^(m_split − lse), g·(1 − p_y), y, 0}
+    uint16_t* pbuf;  // NULL = the recompute plan (k_lmloss_dw)
+    int pntt;        // 32-token tiles of the P layout (2·⌈N / 64⌉)
+    f32x4_t* prec;   // [kLLMaxSplits][N] (compact token index)
     int ncu;         // compute units (the forward's split choice, ll_fwd_splits)
     int mode;
     // ---- per-token PPO fields (the names ppo_token.h reads; see RowArgs in vocab_rows.hip)
@@ -397,6 +405,38 @@ __device__ __forceinline__ bf16x8_t ll16_tr_frag(const char* tile, const int* tr
     const s16x4_t hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + 4096));
     const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi4.x, hi4.y, hi4.z, hi4.w};
     return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// ------------------------------------------------------------------ saved P (the dwp plan)
+// The bf16 P tile a 16x16x32 forward wave just formed (lane (g, c): token c of the wave's 16,
+// vocab rows 16mb + 4g + r of tile t, element 4mb + r) goes to HBM in the layout the dW kernel
+// consumes as its A operand, so k_lmloss_dwp loads one 16-B chunk per lane and never recomputes
+// S:  pbuf[vb = t/2][token tile tt][dW wave 2(t&1) + hv][dW lane (g, c)][16 B] holds vocab row
+// 16hv + c of the tile for tokens 8g..8g+7 of the 32-token tile (k_lmloss_dwp's k slots: slot j
+// of lane group g = token 8g + j).  Lane groups g = 2·half, 2·half + 1 come from the forward
+// wave holding the tile's tokens 16·half..16·half+15, so every forward lane stores one whole
+// 16-B chunk (512 contiguous bytes per wave and dW wave).  The transpose runs through a
+// per-wave 16 x 32 LDS image (token rows of kLLPRow bytes): two ds_read_b64_tr_b16 give lane
+// (g, c) column 16·(g >> 1) + c, token rows 8·(g & 1) + 0..3 and + 4..7 (T10).
+constexpr int kLLPRow = 72;
+__device__ __forceinline__ s16x8_t ll_p_stage(char* pscr, bf16x8_t pb, int lane) {
+    typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+    const int g = lane >> 4, c = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
+    const s16x8_t v = __builtin_bit_cast(s16x8_t, pb);
+    *reinterpret_cast<s16x4_t*>(pscr + kLLPRow * c + 8 * g) = s16x4_t{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<s16x4_t*>(pscr + kLLPRow * c + 32 + 8 * g) = s16x4_t{v[4], v[5], v[6], v[7]};
+    const char* rd = pscr + kLLPRow * (8 * (g & 1) + q) + 32 * (g >> 1) + 8 * p;
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)rd);
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(rd + 4 * kLLPRow));
+    return s16x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+}
+__device__ __forceinline__ void ll_p_store(const LmLossArgs& a, const s16x8_t& v, int t, int tt, int half,
+                                           int lane) {
+    const int g = lane >> 4, c = lane & 15;
+    char* dst = reinterpret_cast<char*>(a.pbuf) +
+                ((int64_t(t >> 1) * a.pntt + tt) * 4 + 2 * (t & 1) + (g >> 1)) * 1024 +
+                16 * (16 * (2 * half + (g & 1)) + c);
+    *reinterpret_cast<s16x8_t*>(dst) = v;
 }
 
 // Vocab splits of the forward for ntb live token blocks: the count (<= a.nsplit) whose last
@@ -700,16 +740,21 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 //                                     transposed: the A operand; the lane's own 8 P values: B)
 // Software-pipelined one tile deep over a 3-stage ring (S(t+1) beside softmax(t), O(t) beside
 // nothing but tile t+2's DMA).
-template <class G, bool RESTART>
+template <class G, bool RESTART, bool SAVEP>
 __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit,
                                                int nv) {
     constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI, kStage = G::kStage;
     constexpr int NG = 2 * KS;  // S-phase gaps
+    static_assert(NG >= 20, "the P-save gaps");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // SAVEP: this wave's P transpose image (the exchange region, unused by this form) and its
+    // place in the dW layout (ll_p_stage / ll_p_store)
+    char* pscr = smem + 3 * kStage + wave * 4096;
     const int g = lane >> 4, c = lane & 15;
     const int split = lin / ntb, mt = lin - split * ntb;
     const int tm = mt * kLLTokBlock + wave * 16 + c;  // this lane's token (compact index)
+    const int ptt = 2 * mt + (wave >> 1), phalf = wave & 1;
     const bool valid = tm < nv;
     const int tc = valid ? tm : nv - 1;
     const int row = a.rows ? a.rows[tc] : tc;
@@ -772,11 +817,22 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         const int mb = k / KS, ks = k % KS;
         s[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], hf[ks], s[mb], 0, 0, 0);
     };
+#if LL_STAMP
+    unsigned long long stamp[8] = {};
+#endif
     // step t (t + 1 < t1): restrict LDS regions (alias scopes, as ll_fwd_block)
     auto step = [&](const char* __restrict__ cur, const char* __restrict__ nx, char* __restrict__ fut, int t)
                     __attribute__((always_inline)) {
-        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));  // this wave's pieces of tile t+1
+        unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
+        LL_TS(ts0);
+        // this wave's pieces of tile t+1 (SAVEP: the previous step's P store, issued after
+        // them, may still fly — it has this step to land)
+        if (SAVEP && t > t0)
+            __builtin_amdgcn_s_waitcnt(ll_vmcnt(1));
+        else
+            __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));
         ll_lds_barrier();  // every wave's; every wave is done with tile t-1
+        LL_TS(ts1);
         constexpr int PF = 4;
         bf16x8_t af[NG];
 #pragma unroll
@@ -786,10 +842,18 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         s[0] = f32x4_t{};
         s[1] = f32x4_t{};
         bf16x8_t pb;
+        s16x8_t pt;
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
             if (k + PF < NG) af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
             s_mfma(nx, af, k);
+            if (SAVEP && k == 13) {
+                if (kLLAblate & 64) {  // diagnostic: no LDS round trip (wrong layout)
+                    pt = __builtin_bit_cast(s16x8_t, pb);
+                } else {
+                    pt = ll_p_stage(pscr, pb, lane);
+                }
+            }
             if (k == 0) {  // the lane's max + token max (no mask inside the loop: see ll_fwd_block)
                 const float lm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])),
                                        fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
@@ -806,6 +870,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             if ((k & 3) == 1 && (k >> 2) < NI) issue_piece(t + 2, fut, k >> 2);
             __builtin_amdgcn_sched_barrier(0);
         }
+        LL_TS(ts2);
         // ---- O(t): tr reads of tile t's W (cur) | MFMA
         constexpr int PFO = 4;
         bf16x8_t tf[DB];
@@ -819,6 +884,16 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             if ((gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 2, fut, gk >> 2);
             __builtin_amdgcn_sched_barrier(0);
         }
+        static_assert(4 * (NI - 1) + 1 < NG, "every DMA piece before the P store (the step's counted wait)");
+        if (SAVEP && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);
+        LL_TS(ts3);
+#if LL_STAMP
+        stamp[0] += ts1 - ts0;
+        stamp[1] += ts2 - ts1;
+        stamp[2] += ts3 - ts2;
+        stamp[6] += 1;
+#endif
+        (void)ts0, (void)ts1, (void)ts2, (void)ts3;
     };
     if (t0 < t1) {
         char* c0 = smem;
@@ -851,7 +926,12 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
 #pragma unroll
         for (int nb = 0; nb < DB; ++nb)
             O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ll16_tr_frag(c0, trb, nb), pb, O[nb], 0, 0, 0);
+        if (SAVEP) ll_p_store(a, ll_p_stage(pscr, pb, lane), t1 - 1, ptt, phalf, lane);
     }
+#if LL_STAMP
+    if (!RESTART && lane == 0 && lin * 4 + wave < (1 << 12))
+        for (int k = 0; k < 8; ++k) g_ll_stamps[(lin * 4 + wave) * 8 + k] = stamp[k];
+#endif
     // per-wave overflow flag (ll_fwd_block); the token's true max and Σ over its four lanes
     bool any = false;
     if (!RESTART) {
@@ -875,8 +955,9 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
 // token count (ll_fwd_splits), and each XCD (blockIdx % 8) takes a contiguous run of the
 // split-major order, so the workgroups sharing an L2 stream the same W rows.  The RESTART
 // launch (one workgroup per CU) walks the blocks and reruns the flagged ones.
-template <class G, bool RESTART, bool F16>
+template <class G, bool RESTART, bool F16, bool SAVEP = false>
 __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
+    static_assert(F16 || !SAVEP, "the saved-P layout comes from the 16x16x32 form");
     __shared__ __attribute__((aligned(16))) char smem[3 * G::kStage + G::kWaves * 4096];
     static_assert(3 * G::kStage + G::kWaves * 4096 <= 163840, "forward LDS: 3 stages + exchange");
     const int nv = a.rows ? *a.nrows : a.N;
@@ -888,7 +969,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
         const int kx = int(blockIdx.x) >> 3, lin = (int(blockIdx.x) & 7) * per_xcd + kx;
         if (kx >= per_xcd || lin >= total) return;  // past an XCD's share / the live tokens
         if (F16)
-            ll_fwd16_block<G, false>(a, smem, lin, ntb, nsplit, nv);
+            ll_fwd16_block<G, false, SAVEP>(a, smem, lin, ntb, nsplit, nv);
         else
             ll_fwd_block<G, false>(a, smem, lin, ntb, nsplit, nv);
         return;
@@ -899,7 +980,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
         for (int w = 0; w < G::kWaves; ++w) f |= a.flags[lin * G::kWaves + w];
         if (!f) continue;
         if (F16)
-            ll_fwd16_block<G, true>(a, smem, lin, ntb, nsplit, nv);
+            ll_fwd16_block<G, true, SAVEP>(a, smem, lin, ntb, nsplit, nv);
         else
             ll_fwd_block<G, true>(a, smem, lin, ntb, nsplit, nv);
         ll_lds_barrier();  // every wave is done with the LDS before the next block reuses it
@@ -995,6 +1076,15 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
         if (MODE == kLLPpo) {
             PolicyTerms pt;
             g = ppo_policy_dlp(lp, p.olp, p.A, p.m, p.inv_msum, a.cliprange, pt);
+            if (a.prec && d4 < nsplit) {
+                // the saved-P plan: split d4's record, dS = (y == v) ? g·(1 − p_y) : −g·e^(m_s − lse)·P
+                float ms = ml[0].x;
+#pragma unroll
+                for (int s = 1; s < kLLMaxSplits; ++s) ms = d4 == s ? ml[s].x : ms;
+                const float q = ms == -INFINITY ? 0.0f : g * exp2_fast((ms - lse) * kLog2e);
+                const float dlab = fmaf(-g, exp2_fast(lp * kLog2e), g);
+                a.prec[int64_t(d4) * a.N + m] = f32x4_t{q, dlab, __int_as_float(yok ? int(y) : -1), 0.0f};
+            }
             if (d4 == 0) {
                 const bool masked = p.m == 0.0f;
                 a.lp_out[row] = masked ? 0.0f : lp;
@@ -1246,6 +1336,272 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
             }
         }
     }
+}
+
+// ------------------------------------------------------------------ dW from the saved P
+// k_lmloss_dw without its Sᵀ pass: the forward left every bf16 P tile in HBM in this kernel's
+// A-operand layout (ll_p_stage / ll_p_store) and the combine a record per (split, token)
+// {q = g·e^(m_split − lse), dlab = g·(1 − p_y), y}, so dS = (y == v) ? dlab : −q·P — the P of the
+// E product rescaled to the final lse, the label entry from the fp32 label logit.  Workgroup =
+// 64·RW vocab rows (4 waves x 16·RW rows over the whole H; dW accumulators 192·RW registers at
+// H = 768) x one token split; per 32-token tile ONE product, dW += dS·h_tile (RW x H/16 MFMAs
+// v_mfma_f32_16x16x32_bf16; the h tile read transposed, each fragment feeding RW MFMAs: lane
+// group g's k slots = tokens 8g..8g+7, rows 8g + q and 8g + 4 + q of the subtile image —
+// conflict-free on the ll16_swz image).  RW = 2 halves the h bytes staged and read from LDS per
+// MFMA (the RW = 1 form's dW phase ran at ~2.7x its MFMA time, bound by the DMA issue and the
+// LDS reads).  The dS of the NEXT tile is formed in the MFMA gaps (records read in two groups
+// of 4, the values after them).  Loads run ahead: a 3-stage h ring (the DMA of tile t+2 during
+// tile t), 3 record slots (tile t+3), P chunks in 3 register sets (tile t+3's load issued at
+// tile t), and the barrier waits only for what was issued before the previous tile (counted
+// vmcnt: P streams from HBM, 0.62 GB per call at C2).
+template <class G, int RW, int HSP>
+__global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
+    // HSP = 2: a workgroup owns HALF the hidden columns of its vocab rows (h part hp = blockIdx
+    // & 1, the two parts of a block adjacent in dispatch order so the second P read hits the
+    // Infinity Cache): RW = 2 then holds 32 rows x H/2 = 192 accumulators, the RW = 1 budget
+    constexpr int H = G::H, HC = H / HSP, DB = HC / 16, NI = G::NI / HSP;
+    constexpr int kStage = G::kStage / HSP;
+    constexpr int kRecSlot = RW == 1 ? 1024 : 4096;  // RW = 2: each wave's own 1-KB records
+    static_assert(G::kWaves == 4, "dW: four waves per workgroup");
+    static_assert(HC % 128 == 0, "h parts of whole 128-column segments");
+    static_assert(3 * kStage + 3 * kRecSlot <= 163840, "3 h stages + 3 record slots");
+    static_assert(4 * (NI - 1) + 1 < DB, "every DMA piece inside the tile's gaps");
+    __shared__ __attribute__((aligned(16))) char smem[3 * kStage + 3 * kRecSlot];
+    char* recs = smem + 3 * kStage;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, c = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
+    const int nv = a.rows ? *a.nrows : a.N;
+    constexpr int vpw = 64 * RW;
+    const int hp = HSP == 1 ? 0 : int(blockIdx.x) & 1, bid = int(blockIdx.x) / HSP;
+    const bool part = bid >= a.dw_full;
+    const int j = bid - a.dw_full;
+    const int vb = part ? a.dw_full + j / a.tsplit : bid;
+    const int ts = part ? j % a.tsplit : 0, nts = part ? a.tsplit : 1;
+    const int r0 = vb * vpw + wave * 16 * RW;  // this wave's first vocab row
+    const int ntt = (nv + kLLRows - 1) / kLLRows;
+    const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
+    // the forward's split of the vocab tiles (ll_fwd_splits: the same plan)
+    const int nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
+    const int nvt = (a.V + kLLRows - 1) / kLLRows;
+    auto split_of = [&](int vt) {
+        int s = 0;
+        for (int k = 1; k < nsplit; ++k) s = int(int64_t(k) * nvt / nsplit) <= vt ? k : s;
+        return s;
+    };
+    // the records this lane DMAs and where the wave reads its tokens' records (+ 16·j)
+    const int srec = RW == 1 ? split_of(2 * vb + (lane >> 5)) : split_of(4 * vb + wave);
+    const int rdst = RW == 1 ? 0 : 1024 * wave;
+    const int rb16 = (RW == 1 ? 512 * (wave >> 1) : 1024 * wave) + 16 * (8 * g);
+    // transposed reads of the h tile: rows 8g + 4hf + q, columns 16nb + 4p (ll_off image)
+    int trb8[2][2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+            trb8[par][hf] = 2048 * g + 64 * (4 * hf + q) + 16 * ((2 * par + (p >> 1)) ^ ll16_swz((2 * g + hf) & 3)) +
+                            8 * (p & 1);
+    auto tr_frag = [&](const char* tile, int nb) __attribute__((always_inline)) {
+        typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+        const int off = (nb >> 3) * 8192 + ((nb & 7) >> 1) * 512;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(tile + trb8[nb & 1][0] + off));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(tile + trb8[nb & 1][1] + off));
+        const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        return __builtin_bit_cast(bf16x8_t, v);
+    };
+    auto tok_row = [&](int m) { return m < nv ? (a.rows ? a.rows[m] : m) : a.N; };
+    const int rA = ll_piece_row(wave, lane), rB = ll_piece_row(wave + G::kWaves, lane);
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.h, uint32_t(int64_t(a.N) * a.ldh * 2));
+    const __amdgpu_buffer_rsrc_t rrec = make_rsrc(a.prec, uint32_t(kLLMaxSplits) * uint32_t(a.N) * 16u);
+    const __amdgpu_buffer_rsrc_t rrows = make_rsrc(a.rows, a.rows ? uint32_t(a.N) * 4u : 0u);
+    auto stage = [&](int t) __attribute__((always_inline)) { return smem + (t % 3) * kStage; };
+    auto rslot = [&](int t) __attribute__((always_inline)) { return recs + (t % 3) * kRecSlot; };
+    // piece il of the part's image = piece hp·HC/16 + il of the full-H image (a multiple of 8:
+    // the same rows)
+    auto issue_piece = [&](int t, char* slot, int k, int ra, int rbw) __attribute__((always_inline)) {
+        const int il = wave + G::kWaves * k, i = hp * (HC / 16) + il;
+        const int rbytes = int(__umul24(uint32_t(((il & 7) == (wave & 7)) ? ra : rbw), uint32_t(a.ldh) * 2u));
+        const int off = ll16_piece_src(i, rbytes, lane);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + il * 1024), 16,
+                                                 t < t1 ? off : int(0x7ffff000), 0, 0, 0);
+    };
+    // records of tile t: lane l -> split srec, token t·32 + (l & 31), at byte rdst + 16·l of the
+    // slot (RW = 1: lanes 32-63 the block's second vocab tile, every wave the same DMA; RW = 2:
+    // each wave its own tile's, lanes 32-63 a copy); zero past the live tokens (q = dlab = 0:
+    // dS = 0 whatever P holds there).  No wave-dependent branch: every wave's count of loads in
+    // flight is the same and the counted waits stay exact.
+    auto issue_recs = [&](int t, char* slot) __attribute__((always_inline)) {
+        const int m = t * kLLRows + (lane & 31);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rrec, (__attribute__((address_space(3))) void*)(slot + rdst), 16,
+                                                 t < t1 && m < nv ? (srec * a.N + m) * 16 : int(0x7ffffff0), 0, 0,
+                                                 0);
+    };
+    // P chunk of tile t for row half hh (rows r0 + 16hh + c, tokens 8g..8g+7), clamped to the
+    // split's last tile: 64-row block (r0 + 16hh) / 64, dW wave slot ((r0 + 16hh) / 16) & 3
+    const s16x8_t* pbase[RW];
+#pragma unroll
+    for (int hh = 0; hh < RW; ++hh) {
+        const int rr0 = r0 + 16 * hh;
+        pbase[hh] = reinterpret_cast<const s16x8_t*>(a.pbuf) + (int64_t(rr0 >> 6) * a.pntt * 4 + ((rr0 >> 4) & 3)) * 64 +
+                    lane;
+    }
+    auto load_p = [&](int t, int hh) __attribute__((always_inline)) {
+        return pbase[hh][int64_t(min(t, t1 - 1)) * 256];
+    };
+    auto ds_of = [&](const f32x4_t& rec, short pe, int vcol) __attribute__((always_inline)) {
+        const float pv = __uint_as_float(uint32_t(uint16_t(pe)) << 16);
+        return __float_as_int(rec.z) == vcol ? rec.y : -rec.x * pv;
+    };
+    auto rec_at = [&](const char* slot, int e) __attribute__((always_inline)) {
+        return *reinterpret_cast<const f32x4_t*>(slot + rb16 + 16 * e);
+    };
+    f32x4_t D[RW][DB];  // dW[r0 + 16hh + 4g + r][16nb + c]
+#pragma unroll
+    for (int hh = 0; hh < RW; ++hh)
+#pragma unroll
+        for (int nb = 0; nb < DB; ++nb) D[hh][nb] = f32x4_t{};
+    bf16x8_t da[RW];
+    s16x8_t R0[RW], R1[RW], R2[RW];  // P(t0 + k) in R[k % 3]
+#pragma unroll
+    for (int hh = 0; hh < RW; ++hh) {
+        da[hh] = bf16x8_t{};
+        R0[hh] = R1[hh] = R2[hh] = s16x8_t{};
+    }
+    int nrowA = 0, nrowB = 0;  // rows of tile t+2 at the start of tile t
+    if (t0 < t1) {
+        const int rowA0 = tok_row(t0 * kLLRows + rA), rowB0 = tok_row(t0 * kLLRows + rB);
+        const int rowA1 = tok_row((t0 + 1) * kLLRows + rA), rowB1 = tok_row((t0 + 1) * kLLRows + rB);
+        nrowA = a.rows ? a.rows[min((t0 + 2) * kLLRows + rA, nv - 1)] : 0;
+        nrowB = a.rows ? a.rows[min((t0 + 2) * kLLRows + rB, nv - 1)] : 0;
+#pragma unroll
+        for (int hh = 0; hh < RW; ++hh) {
+            R0[hh] = load_p(t0, hh);
+            R1[hh] = load_p(t0 + 1, hh);
+            R2[hh] = load_p(t0 + 2, hh);
+        }
+#pragma unroll
+        for (int k = 0; k < NI; ++k) issue_piece(t0, stage(t0), k, rowA0, rowB0);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) issue_piece(t0 + 1, stage(t0 + 1), k, rowA1, rowB1);
+        issue_recs(t0, rslot(t0));
+        issue_recs(t0 + 1, rslot(t0 + 1));
+        issue_recs(t0 + 2, rslot(t0 + 2));
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));
+        ll_lds_barrier();
+#pragma unroll
+        for (int hh = 0; hh < RW; ++hh) {
+            float ds[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ds[e] = ds_of(rec_at(rslot(t0), e), R0[hh][e], r0 + 16 * hh + c);
+            da[hh] = pack8(ds);
+        }
+    }
+#if LL_STAMP
+    unsigned long long stamp[8] = {};
+#endif
+    // tile t: dW(t) with da = dS(t); in its gaps the loads of the tiles ahead and dS(t+1) from
+    // puse = P(t+1) and the records of t+1 (rnx); pnew receives P(t+3).  The LDS regions are
+    // __restrict__ parameters (alias scopes: the DMA targets fut / rfut apart from the regions
+    // read, as k_lmloss_dw — without them hipcc waits for the DMA before every read).
+    auto tile_body = [&](const char* __restrict__ cur, char* __restrict__ fut, const char* __restrict__ rnx,
+                         char* __restrict__ rfut, int t, const s16x8_t (&puse)[RW], s16x8_t (&pnew)[RW])
+                         __attribute__((always_inline)) {
+        const int ma = (t + 2) * kLLRows + rA, mb1 = (t + 2) * kLLRows + rB;  // tile t+2's rows
+        const int pa = ma < nv ? (a.rows ? nrowA : ma) : a.N;
+        const int pb = mb1 < nv ? (a.rows ? nrowB : mb1) : a.N;
+        nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rA, nv - 1) * 4, 0, 0);
+        nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rB, nv - 1) * 4, 0, 0);
+        if (!(kLLAblate & 128)) {
+#pragma unroll
+            for (int hh = 0; hh < RW; ++hh) pnew[hh] = load_p(t + 3, hh);
+        }
+        bf16x8_t dn[RW];
+        f32x4_t rr[4];
+        float dsn[RW][8];
+        // gaps: the records of tokens 0-3 read at kR0, their dS at kD0 (L gaps ≈ 128 MFMA cycles
+        // later); tokens 4-7 at kR1 / kD1; the pack at kPk
+        constexpr int PFO = 4, L = 8 / RW, kR0 = 1, kD0 = kR0 + L, kR1 = kD0 + 1, kD1 = kR1 + L, kPk = kD1 + 1;
+        static_assert(kPk < DB, "the dS gaps");
+        bf16x8_t tf[DB];
+#pragma unroll
+        for (int nb = 0; nb < PFO; ++nb) tf[nb] = tr_frag(cur, nb);
+#pragma unroll
+        for (int nb = 0; nb < DB; ++nb) {
+            if (nb + PFO < DB) tf[nb + PFO] = tr_frag(cur, nb + PFO);
+#pragma unroll
+            for (int hh = 0; hh < RW; ++hh)
+                D[hh][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[hh], tf[nb], D[hh][nb], 0, 0, 0);
+            if ((nb & 3) == 1 && (nb >> 2) < NI && !(kLLAblate & 256)) issue_piece(t + 2, fut, nb >> 2, pa, pb);
+            if (nb == 2) issue_recs(t + 3, rfut);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (nb == kR0) rr[e] = rec_at(rnx, e);
+                if (nb == kR1) rr[e] = rec_at(rnx, 4 + e);
+            }
+#pragma unroll
+            for (int hh = 0; hh < RW; ++hh) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (nb == kD0) dsn[hh][e] = ds_of(rr[e], puse[hh][e], r0 + 16 * hh + c);
+                    if (nb == kD1) dsn[hh][4 + e] = ds_of(rr[e], puse[hh][4 + e], r0 + 16 * hh + c);
+                }
+                if (nb == kPk) dn[hh] = pack8(dsn[hh]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (!(kLLAblate & 512)) {
+#pragma unroll
+            for (int hh = 0; hh < RW; ++hh) da[hh] = dn[hh];
+        }
+    };
+    auto tile = [&](int t, const s16x8_t (&puse)[RW], s16x8_t (&pnew)[RW]) __attribute__((always_inline)) {
+        unsigned long long ts0 = 0, ts1 = 0, ts2 = 0;
+        LL_TS(ts0);
+        // everything issued before the previous tile (2 row indices, RW P chunks, NI pieces, the
+        // records: NI + 3 + RW per tile): h(t), the records and P of t+1
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI + 3 + RW));
+        ll_lds_barrier();
+        LL_TS(ts1);
+        tile_body(stage(t), stage(t + 2), rslot(t + 1), rslot(t + 3), t, puse, pnew);
+        LL_TS(ts2);
+#if LL_STAMP
+        stamp[0] += ts1 - ts0;
+        stamp[3] += ts2 - ts1;
+        stamp[6] += 1;
+#endif
+        (void)ts0, (void)ts1, (void)ts2;
+    };
+    for (int t = t0; t < t1; t += 3) {
+        tile(t, R1, R0);
+        if (t + 1 < t1) tile(t + 1, R2, R1);
+        if (t + 2 < t1) tile(t + 2, R0, R2);
+    }
+#if LL_STAMP
+    if (lane == 0 && blockIdx.x * 4 + wave < (1 << 12))
+        for (int k = 0; k < 8; ++k) g_ll_stamps[(1 << 15) + (blockIdx.x * 4 + wave) * 8 + k] = stamp[k];
+#endif
+#pragma unroll
+    for (int hh = 0; hh < RW; ++hh)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int vr = wave * 16 * RW + 16 * hh + 4 * g + r, v = vb * vpw + vr;
+            if (part) {
+                float* out = a.dwpart + (int64_t(j) * vpw + vr) * H + hp * HC + c;
+#pragma unroll
+                for (int nb = 0; nb < DB; ++nb) out[16 * nb] = D[hh][nb][r];
+            } else if (v < a.V) {
+                const int64_t o = int64_t(v) * a.lddw + hp * HC + c;
+                if (a.dw_dtype == TRLX_F32) {
+                    float* out = static_cast<float*>(a.dw) + o;
+#pragma unroll
+                    for (int nb = 0; nb < DB; ++nb) out[16 * nb] = D[hh][nb][r];
+                } else {
+                    uint16_t* out = static_cast<uint16_t*>(a.dw) + o;
+#pragma unroll
+                    for (int nb = 0; nb < DB; ++nb) out[16 * nb] = f2bf(D[hh][nb][r]);
+                }
+            }
+        }
 }
 
 // Fixed-order sum of the token-split dW partials of the vocab blocks past dw_full:
@@ -1886,7 +2242,7 @@ __device__ __forceinline__ void hs8_engine(const LmLossArgs& a, char* smem, cons
             acc[0] = f32x4_t{};
             acc[1] = f32x4_t{};
         }
-        bf16x8_t xsf;
+        bf16x8_t xsf = bf16x8_t{};
         if (DP) xsf = *reinterpret_cast<const bf16x8_t*>(xsr_p + xsr);
         float2 xv[4];
         f32x4_t rec[2];
@@ -2223,21 +2579,32 @@ __global__ __launch_bounds__(512, 2) void k_lmloss_fwd_hs8(LmLossArgs a) {
 // ------------------------------------------------------------------ host side
 static TuneKnob g_ll_splits{0};  // tuning "lmloss_splits" (0 = auto)
 static TuneKnob g_ll_tsplit{0};  // tuning "lmloss_dw_tsplit" (0 = auto)
-// tuning "lmloss_fwd": 0 auto (= 1), 1 the 32x32x16 pair form (ll_fwd_block), 2 the 16x16x32 form
-// (ll_fwd16_block: no exchange, but twice the LDS bytes per MFMA — measured 1123 vs ~1010 us
-// at C2, while the same trade won for dW, whose exchange and dS sat on the critical path),
-// 3 the H-sliced form (k_lmloss_fwd_hs)
+// tuning "lmloss_fwd": 0 auto (= 2), 1 the 32x32x16 pair form (ll_fwd_block), 2 the 16x16x32 form
+// (ll_fwd16_block: no exchange; since the conflict-free image of round 4 the faster one —
+// interleaved A/B C2 917-921 vs 938-941 us, C3 625 vs 642 us, profiles/r05b_forms_*), 3 the
+// H-sliced form (k_lmloss_fwd_hs), 4 its 8-wave variant (k_lmloss_fwd_hs8).  The saved-P plan
+// always runs form 2 (the P layout is that form's).
 static TuneKnob g_ll_fwd{0};
-// tuning "lmloss_dw": 0 auto (= 1), 1 the row-split 16x16x32 form (k_lmloss_dw), 2 the H-sliced
-// form (k_lmloss_dw_hs)
+// tuning "lmloss_dw": 0 auto (= 4 where the caller's workspace holds the saved P — the PPO
+// entries given trlx_ppo_loss_from_hidden_workspace_bytes — else 1), 1 the row-split 16x16x32
+// form (k_lmloss_dw: Sᵀ recomputed), 2 / 3 the H-sliced forms (k_lmloss_dw_hs / _hs8), 4 the
+// saved-P plan (k_lmloss_dwp; falls back to 1 when the workspace is too small)
 static TuneKnob g_ll_dw{0};
+// tuning "lmloss_dwp_rw": the saved-P dW kernel's vocab rows per wave, 16·RW (0 auto = 2, 1, 2)
+static TuneKnob g_ll_rw{0};
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
     const bool sp = key && !__builtin_strcmp(key, "lmloss_splits");
     const bool ts = key && !__builtin_strcmp(key, "lmloss_dw_tsplit");
     const bool fw = key && !__builtin_strcmp(key, "lmloss_fwd");
     const bool dwk = key && !__builtin_strcmp(key, "lmloss_dw");
-    *handled = sp || ts || fw || dwk;
+    const bool rwk = key && !__builtin_strcmp(key, "lmloss_dwp_rw");
+    *handled = sp || ts || fw || dwk || rwk;
+    if (rwk) {
+        TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "lmloss_dwp_rw: 0 auto, 1, 2");
+        g_ll_rw = int(value);
+        return TRLX_OK;
+    }
     if (fw) {
         TRLX_REQUIRE(value >= 0 && value <= 4, TRLX_ERR_ARG,
                      "lmloss_fwd: 0 auto, 1 32x32 pair form, 2 16x16 form, 3 H-sliced form, 4 H-sliced 8-wave form");
@@ -2245,8 +2612,8 @@ int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
         return TRLX_OK;
     }
     if (dwk) {
-        TRLX_REQUIRE(value >= 0 && value <= 3, TRLX_ERR_ARG,
-                     "lmloss_dw: 0 auto, 1 row-split form, 2 H-sliced form, 3 H-sliced 8-wave form");
+        TRLX_REQUIRE(value >= 0 && value <= 4, TRLX_ERR_ARG,
+                     "lmloss_dw: 0 auto, 1 row-split form, 2 H-sliced form, 3 H-sliced 8-wave form, 4 saved P");
         g_ll_dw = int(value);
         return TRLX_OK;
     }
@@ -2270,6 +2637,8 @@ struct LlWs {
     int* cnt;
     int* flags;
     float* dwpart;
+    uint16_t* pbuf;  // saved-P plan only
+    f32x4_t* prec;
 };
 // Compute units of the current device (the grid plans below).
 static int ll_ncu() {
@@ -2291,9 +2660,9 @@ static int ll_ncu() {
 struct LlDwPlan {
     int full, tsplit, nblk;  // workgroups = full + nblk·tsplit
 };
-static LlDwPlan ll_dw_plan(int64_t V) {
+static LlDwPlan ll_dw_plan(int64_t V, int vpw = kLLTokBlock) {
     const int ncu = ll_ncu();
-    const int nvb = int((V + kLLTokBlock - 1) / kLLTokBlock);
+    const int nvb = int((V + vpw - 1) / vpw);
     const int rem = nvb % ncu;
     LlDwPlan p{nvb, 1, 0};
     if (g_ll_tsplit == 1 || rem == 0) return p;
@@ -2305,9 +2674,13 @@ static LlDwPlan ll_dw_plan(int64_t V) {
     return p;
 }
 
+// 32-token tiles of the saved-P layout: the forward's 64-token blocks, whole
+static int ll_pntt(int64_t N) { return int(2 * ((N + kLLTokBlock - 1) / kLLTokBlock)); }
+
 // Workspace carve-up for N tokens (dwpart: the split blocks' fp32 partials).
 // fwd = false: the backward's carve-up (trlx_lmhead_logprobs_bwd), no forward partials.
-static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, bool fwd = true) {
+// savep: + the saved-P plan's P tiles (⌈V/64⌉ x 2⌈N/64⌉ x 4 KB: 0.62 GB at C2) and records.
+static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, bool fwd = true, bool savep = false) {
     char* p = static_cast<char*>(base);
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -2322,8 +2695,11 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, boo
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t(order_chunks(N) + 1) * 4));
     t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 8 * 4));  // <= 8 waves per workgroup
-    const LlDwPlan dp = ll_dw_plan(V);
-    t.dwpart = reinterpret_cast<float*>(take(size_t(dp.nblk) * dp.tsplit * kLLTokBlock * H * 4));
+    const LlDwPlan dp = ll_dw_plan(V), dp2 = ll_dw_plan(V, 2 * kLLTokBlock);  // 64- / 128-row blocks
+    t.dwpart = reinterpret_cast<float*>(take(std::max(size_t(dp.nblk) * dp.tsplit * kLLTokBlock,
+                                                      size_t(dp2.nblk) * dp2.tsplit * 2 * kLLTokBlock) * H * 4));
+    t.pbuf = reinterpret_cast<uint16_t*>(take(savep ? size_t((V + 63) / 64) * ll_pntt(N) * 4096 : 0));
+    t.prec = reinterpret_cast<f32x4_t*>(take(savep ? size_t(kLLMaxSplits) * N * 16 : 0));
     if (w) *w = t;
     return off;
 }
@@ -2354,7 +2730,7 @@ template <class G, class HG, class H8>
 static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
     const int64_t ntb = (a.N + kLLTokBlock - 1) / kLLTokBlock;
     const unsigned grid = unsigned((ntb * a.nsplit + 7) / 8 * 8);
-    if (g_ll_fwd == 4) {
+    if (g_ll_fwd == 4 && !a.pbuf) {
         hipLaunchKernelGGL((k_lmloss_fwd_hs8<H8, false>), dim3(grid), dim3(512), 0, s, a);
         const int rc = check_launch("k_lmloss_fwd_hs8");
         if (rc) return rc;
@@ -2362,7 +2738,7 @@ static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
                            s, a);
         return check_launch("k_lmloss_fwd_hs8 restart");
     }
-    if (g_ll_fwd == 3) {
+    if (g_ll_fwd == 3 && !a.pbuf) {
         hipLaunchKernelGGL((k_lmloss_fwd_hs<HG, false>), dim3(grid), dim3(256), 0, s, a);
         const int rc = check_launch("k_lmloss_fwd_hs");
         if (rc) return rc;
@@ -2370,9 +2746,13 @@ static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
                            s, a);
         return check_launch("k_lmloss_fwd_hs restart");
     }
-    const bool f16 = g_ll_fwd == 2;
-    void (*first)(LmLossArgs) = f16 ? k_lmloss_fwd<G, false, true> : k_lmloss_fwd<G, false, false>;
-    void (*restart)(LmLossArgs) = f16 ? k_lmloss_fwd<G, true, true> : k_lmloss_fwd<G, true, false>;
+    const bool f16 = g_ll_fwd == 0 || g_ll_fwd == 2;
+    void (*first)(LmLossArgs) = a.pbuf ? k_lmloss_fwd<G, false, true, true>
+                                : f16  ? k_lmloss_fwd<G, false, true>
+                                       : k_lmloss_fwd<G, false, false>;
+    void (*restart)(LmLossArgs) = a.pbuf ? k_lmloss_fwd<G, true, true, true>
+                                  : f16  ? k_lmloss_fwd<G, true, true>
+                                         : k_lmloss_fwd<G, true, false>;
     hipLaunchKernelGGL(first, dim3(grid), dim3(G::kThreads), 0, s, a);
     const int rc = check_launch("k_lmloss_fwd");
     if (rc) return rc;
@@ -2382,6 +2762,13 @@ static int ll_launch_fwd(const LmLossArgs& a, hipStream_t s) {
 template <class G, class HG, class H8>
 static int ll_launch_dw(const LmLossArgs& a, hipStream_t s) {
     const dim3 grid(unsigned(a.dw_full + a.dw_nblk * a.tsplit));
+    if (a.pbuf) {
+        if (a.dw_vpw == 2 * kLLTokBlock)  // 128 rows x H/2 per workgroup: two per vocab block
+            hipLaunchKernelGGL((k_lmloss_dwp<G, 2, 2>), dim3(2 * grid.x), dim3(G::kThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_lmloss_dwp<G, 1, 1>), grid, dim3(G::kThreads), 0, s, a);
+        return check_launch("k_lmloss_dwp");
+    }
     if (g_ll_dw == 3) {
         hipLaunchKernelGGL(k_lmloss_dw_hs8<H8>, grid, dim3(512), 0, s, a);
         return check_launch("k_lmloss_dw_hs8");
@@ -2404,7 +2791,7 @@ static int ll_dw(const LmLossArgs& a, hipStream_t s) {
 static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                     int64_t H, int64_t V, const int64_t* labels, int64_t lb, const int64_t* compact_mask,
                     void* lm_ws, void* dweight, int dw_dtype, int64_t lddw, LlWs& w, hipStream_t s,
-                    bool fwd = true) {
+                    bool fwd = true, bool savep = false) {
     int rc = ll_check(hidden, ldh, weight, ldw, N, H, V);
     if (rc) return rc;
     TRLX_REQUIRE(labels && lm_ws, TRLX_ERR_ARG, "NULL labels / workspace");
@@ -2420,12 +2807,16 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.nsplit = g_ll_splits ? g_ll_splits : kLLMaxSplits;
     a.nsplit_fixed = g_ll_splits != 0;
     a.ncu = ll_ncu();
-    const LlDwPlan dp = ll_dw_plan(V);
+    a.dw_vpw = savep && g_ll_rw != 1 ? 2 * kLLTokBlock : kLLTokBlock;
+    const LlDwPlan dp = ll_dw_plan(V, a.dw_vpw);
     a.dw_full = dp.full;
     a.tsplit = dp.tsplit;
     a.dw_nblk = dp.nblk;
-    ll_carve(lm_ws, N, H, V, &w, fwd);
+    ll_carve(lm_ws, N, H, V, &w, fwd, savep);
     a.dwpart = w.dwpart;
+    a.pbuf = savep ? w.pbuf : nullptr;
+    a.pntt = ll_pntt(N);
+    a.prec = savep ? w.prec : nullptr;
     a.opart = w.opart;
     a.mlpart = w.mlpart;
     a.trec = w.trec;
@@ -2450,7 +2841,7 @@ static int ll_dw_finish(const LmLossArgs& a, void* dweight, int dw_dtype, int64_
     int rc = ll_dw(a, s);
     if (rc || a.dw_nblk == 0) return rc;
     hipLaunchKernelGGL(k_lmloss_dw_reduce, dim3(1024), dim3(256), 0, s, w.dwpart, a.tsplit, a.dw_nblk, a.dw_full,
-                       kLLTokBlock, dweight, dw_dtype, a.V, a.H, lddw);
+                       a.dw_vpw, dweight, dw_dtype, a.V, a.H, lddw);
     return check_launch("k_lmloss_dw_reduce");
 }
 
@@ -2466,6 +2857,10 @@ extern "C" int64_t trlx_lmhead_loss_bwd_workspace_bytes(int64_t N, int64_t H, in
     return int64_t(ll_carve(nullptr, N, H, V, nullptr, false));
 }
 
+extern "C" int64_t trlx_ppo_loss_from_hidden_workspace_bytes(int64_t N, int64_t H, int64_t V) {
+    return int64_t(ll_carve(nullptr, N, H, V, nullptr, true, true));
+}
+
 // The PPO loss side from hidden states, once `a` holds the per-token PPO fields (whitening by
 // the unsplit record or the split-beta coefficients): shapes, compaction, the three MFMA
 // launches and the combine.
@@ -2474,7 +2869,7 @@ static int ll_ppo_loss(LmLossArgs& a, const void* hidden, int64_t ldh, const voi
                        const void* values, int v_dtype, const void* old_values, int ov_dtype, const void* returns,
                        int r_dtype, float cliprange, float cliprange_value, float vf_coef, float* lp_out,
                        void* dhidden, int64_t lddh, int dh_dtype, void* dweight, int dw_dtype, int64_t lddw,
-                       float* dvalues, void* workspace, void* lm_workspace, hipStream_t s) {
+                       float* dvalues, void* workspace, void* lm_workspace, int64_t lm_bytes, hipStream_t s) {
     LlWs w;
     const int64_t N = B * T;
     TRLX_REQUIRE(B > 0 && T > 0, TRLX_ERR_SHAPE, "empty rollout batch");
@@ -2488,8 +2883,14 @@ static int ll_ppo_loss(LmLossArgs& a, const void* hidden, int64_t ldh, const voi
     // only the all-ones mask (N) is known here
     TRLX_REQUIRE(a.msum || !mask, TRLX_ERR_ARG,
                  "trlx_ppo_loss_from_hidden: a mask needs the GAE record (its Σ mask normalises the loss)");
+    // the plan the caller's workspace holds: the saved-P plan (trlx_ppo_loss_from_hidden_workspace_bytes)
+    // unless tuned off, else the recompute plan (trlx_lmhead_loss_workspace_bytes)
+    TRLX_REQUIRE(lm_bytes >= int64_t(ll_carve(nullptr, N, H, V, nullptr)), TRLX_ERR_ARG,
+                 "lm_workspace of %lld bytes: below trlx_lmhead_loss_workspace_bytes(%lld, %lld, %lld)",
+                 (long long)lm_bytes, (long long)N, (long long)H, (long long)V);
+    const bool savep = (g_ll_dw == 0 || g_ll_dw == 4) && lm_bytes >= int64_t(ll_carve(nullptr, N, H, V, nullptr, true, true));
     int rc = ll_setup(a, hidden, ldh, weight, ldw, N, H, V, labels, 1, mask, lm_workspace, dweight, dw_dtype, lddw, w,
-                      s);
+                      s, true, savep);
     if (rc) return rc;
     Workspace ws;
     carve_ppo_workspace(workspace, B, T, &ws);
@@ -2525,7 +2926,7 @@ extern "C" int trlx_ppo_loss_from_hidden(
     const int64_t* mask, const void* values, int v_dtype, const void* old_values, int ov_dtype, const void* returns,
     int r_dtype, float cliprange, float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh,
     int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, float* dvalues, void* workspace, void* lm_workspace,
-    void* stream) {
+    int64_t lm_workspace_bytes, void* stream) {
     LmLossArgs a = {};
     TRLX_REQUIRE(adv_raw, TRLX_ERR_ARG, "NULL adv_raw");
     a.old_lp = old_lp;
@@ -2536,7 +2937,7 @@ extern "C" int trlx_ppo_loss_from_hidden(
     a.msum = stats ? stats + 3 : nullptr;
     return ll_ppo_loss(a, hidden, ldh, weight, ldw, B, T, H, V, labels, mask, values, v_dtype, old_values, ov_dtype,
                        returns, r_dtype, cliprange, cliprange_value, vf_coef, lp_out, dhidden, lddh, dh_dtype, dweight,
-                       dw_dtype, lddw, dvalues, workspace, lm_workspace, (hipStream_t)stream);
+                       dw_dtype, lddw, dvalues, workspace, lm_workspace, lm_workspace_bytes, (hipStream_t)stream);
 }
 
 extern "C" int trlx_ppo_loss_from_hidden_split(
@@ -2546,7 +2947,8 @@ extern "C" int trlx_ppo_loss_from_hidden_split(
     const double* ctl_state, float kl_coef, float* coef_out, const double* msum, const int64_t* mask,
     const void* values, int v_dtype, const void* old_values, int ov_dtype, float* rewards, void* returns, int r_dtype,
     float cliprange, float cliprange_value, float vf_coef, float* lp_out, void* dhidden, int64_t lddh, int dh_dtype,
-    void* dweight, int dw_dtype, int64_t lddw, float* dvalues, void* workspace, void* lm_workspace, void* stream) {
+    void* dweight, int dw_dtype, int64_t lddw, float* dvalues, void* workspace, void* lm_workspace,
+    int64_t lm_workspace_bytes, void* stream) {
     LmLossArgs a = {};
     TRLX_REQUIRE(adv0 && adv_kl && rew_kl && rew_score && rewards, TRLX_ERR_ARG,
                  "NULL split-beta buffer to trlx_ppo_loss_from_hidden_split");
@@ -2569,7 +2971,7 @@ extern "C" int trlx_ppo_loss_from_hidden_split(
     a.msum = msum;
     return ll_ppo_loss(a, hidden, ldh, weight, ldw, B, T, H, V, labels, mask, values, v_dtype, old_values, ov_dtype,
                        returns, r_dtype, cliprange, cliprange_value, vf_coef, lp_out, dhidden, lddh, dh_dtype, dweight,
-                       dw_dtype, lddw, dvalues, workspace, lm_workspace, (hipStream_t)stream);
+                       dw_dtype, lddw, dvalues, workspace, lm_workspace, lm_workspace_bytes, (hipStream_t)stream);
 }
 
 extern "C" int trlx_lmhead_logprobs_fwd_saved(const void* hidden, int64_t ldh, const void* weight, int64_t ldw,

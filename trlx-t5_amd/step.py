@@ -729,7 +729,9 @@ class PPOHotPath:
         if getattr(self, "dhidden", None) is None or self.dhidden.shape != (B, T, H) or self.dhidden.dtype != grad_dtype:
             self.dhidden = torch.empty((B, T, H), dtype=grad_dtype, device=self.device)
             self.dweight = torch.empty((V, H), dtype=grad_dtype, device=self.device)
-        nbytes = _lib.query("trlx_lmhead_loss_workspace_bytes", N, H, V)
+        # the saved-P plan's workspace (the forward's bf16 P tiles: ~V·N·2 bytes, 0.62 GB at C2);
+        # release_loss_workspace() frees it
+        nbytes = _lib.query("trlx_ppo_loss_from_hidden_workspace_bytes", N, H, V)
         if getattr(self, "lm_loss_ws", None) is None or self.lm_loss_ws.numel() < nbytes:
             self.lm_loss_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         s = torch.cuda.current_stream(self.device)
@@ -741,7 +743,8 @@ class PPOHotPath:
                 _lib.dtype_code(old_values))
         outs = (float(self.cfg.cliprange), float(self.cfg.cliprange_value), float(self.cfg.vf_coef),
                 self.lp_new.data_ptr(), dh.data_ptr(), H, _lib.dtype_code(dh), dw.data_ptr(), _lib.dtype_code(dw), H,
-                self.dvalues.data_ptr(), self.workspace.data_ptr(), self.lm_loss_ws.data_ptr(), s.cuda_stream)
+                self.dvalues.data_ptr(), self.workspace.data_ptr(), self.lm_loss_ws.data_ptr(),
+                self.lm_loss_ws.numel(), s.cuda_stream)
         self._ev("loss", s)
         if self._split_mode:
             # split beta (the pipelined DP schedule, or step() with split_beta=True): the
@@ -808,6 +811,10 @@ class PPOHotPath:
     def release_loss_logits(self):
         """Free the policy_loss_from_hidden gemm route's [B, T, V] logits (re-allocated on next use)."""
         self.loss_logits = None
+
+    def release_loss_workspace(self):
+        """Free the fused policy_loss_from_hidden workspace (its saved P tiles; re-allocated on next use)."""
+        self.lm_loss_ws = None
 
     def release_lm_logits(self):
         """Free the gemm route's [2, chunk, T, V] logits ring (re-allocated on next use)."""
