@@ -1516,11 +1516,15 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
             for (int hh = 0; hh < RW; ++hh) pnew[hh] = load_p(t + 3, hh);
         }
         bf16x8_t dn[RW];
-        f32x4_t rr[4];
+        f32x4_t rr[8];
         float dsn[RW][8];
-        // gaps: the records of tokens 0-3 read at kR0, their dS at kD0 (L gaps ≈ 128 MFMA cycles
-        // later); tokens 4-7 at kR1 / kD1; the pack at kPk
-        constexpr int PFO = 4, L = 8 / RW, kR0 = 1, kD0 = kR0 + L, kR1 = kD0 + 1, kD1 = kR1 + L, kPk = kD1 + 1;
+        // gaps: the 8 records read at kR (4 + 4), then one dS value per gap from kD on (L gaps
+        // ≈ 128 MFMA cycles later; one at a time, so the VALU work hides behind the MFMAs of
+        // its gap: four values in one gap had cost ~400 cycles a tile), the packs after them;
+        // transposed reads PFO fragments ahead (≈ 256 MFMA cycles)
+        constexpr int PFO = 8, L = 8 / RW, kR = 1, kD = kR + 1 + L;
+        constexpr int VPG = (8 * RW + (DB - kD - 2)) / (DB - kD - 1);  // dS values per gap
+        constexpr int kPk = kD + (8 * RW + VPG - 1) / VPG;
         static_assert(kPk < DB, "the dS gaps");
         bf16x8_t tf[DB];
 #pragma unroll
@@ -1531,20 +1535,21 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
 #pragma unroll
             for (int hh = 0; hh < RW; ++hh)
                 D[hh][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[hh], tf[nb], D[hh][nb], 0, 0, 0);
+            // (the four waves' pieces in the same gaps: staggering them by wave — a wave-uniform
+            // branch per gap — measured slower in both kernels, the forward's S loop 2,033 ->
+            // 3,900 cycles a tile)
             if ((nb & 3) == 1 && (nb >> 2) < NI && !(kLLAblate & 256)) issue_piece(t + 2, fut, nb >> 2, pa, pb);
             if (nb == 2) issue_recs(t + 3, rfut);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                if (nb == kR0) rr[e] = rec_at(rnx, e);
-                if (nb == kR1) rr[e] = rec_at(rnx, 4 + e);
+                if (nb == kR) rr[e] = rec_at(rnx, e);
+                if (nb == kR + 1) rr[4 + e] = rec_at(rnx, 4 + e);
             }
 #pragma unroll
             for (int hh = 0; hh < RW; ++hh) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (nb == kD0) dsn[hh][e] = ds_of(rr[e], puse[hh][e], r0 + 16 * hh + c);
-                    if (nb == kD1) dsn[hh][4 + e] = ds_of(rr[e], puse[hh][4 + e], r0 + 16 * hh + c);
-                }
+                for (int e = 0; e < 8; ++e)
+                    if (nb == kD + (RW * e + hh) / VPG) dsn[hh][e] = ds_of(rr[e], puse[hh][e], r0 + 16 * hh + c);
                 if (nb == kPk) dn[hh] = pack8(dsn[hh]);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -2660,8 +2665,9 @@ static int ll_ncu() {
 struct LlDwPlan {
     int full, tsplit, nblk;  // workgroups = full + nblk·tsplit
 };
-static LlDwPlan ll_dw_plan(int64_t V, int vpw = kLLTokBlock) {
-    const int ncu = ll_ncu();
+// parts: workgroups per vocab block (the saved-P RW = 2 form's two hidden halves)
+static LlDwPlan ll_dw_plan(int64_t V, int vpw = kLLTokBlock, int parts = 1) {
+    const int ncu = std::max(1, ll_ncu() / parts);
     const int nvb = int((V + vpw - 1) / vpw);
     const int rem = nvb % ncu;
     LlDwPlan p{nvb, 1, 0};
@@ -2695,7 +2701,7 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, boo
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t(order_chunks(N) + 1) * 4));
     t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 8 * 4));  // <= 8 waves per workgroup
-    const LlDwPlan dp = ll_dw_plan(V), dp2 = ll_dw_plan(V, 2 * kLLTokBlock);  // 64- / 128-row blocks
+    const LlDwPlan dp = ll_dw_plan(V), dp2 = ll_dw_plan(V, 2 * kLLTokBlock, 2);  // 64- / 128-row blocks
     t.dwpart = reinterpret_cast<float*>(take(std::max(size_t(dp.nblk) * dp.tsplit * kLLTokBlock,
                                                       size_t(dp2.nblk) * dp2.tsplit * 2 * kLLTokBlock) * H * 4));
     t.pbuf = reinterpret_cast<uint16_t*>(take(savep ? size_t((V + 63) / 64) * ll_pntt(N) * 4096 : 0));
@@ -2808,7 +2814,7 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.nsplit_fixed = g_ll_splits != 0;
     a.ncu = ll_ncu();
     a.dw_vpw = savep && g_ll_rw != 1 ? 2 * kLLTokBlock : kLLTokBlock;
-    const LlDwPlan dp = ll_dw_plan(V, a.dw_vpw);
+    const LlDwPlan dp = ll_dw_plan(V, a.dw_vpw, a.dw_vpw / kLLTokBlock);
     a.dw_full = dp.full;
     a.tsplit = dp.tsplit;
     a.dw_nblk = dp.nblk;
