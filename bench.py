@@ -458,7 +458,11 @@ def from_hidden_leg(torch, P, dev, name, steps, rounds=3):
     nv = int(mask.sum().item()) if masked else B * T
     fused_ms = sorted(times["fused"])[len(times["fused"]) // 2]
     gemm_ms = sorted(times["gemm"])[len(times["gemm"]) // 2]
-    flop = 4 * 2 * nv * V * H  # the fused route's four MFMA passes over the live tokens
+    # the plan the library ran for this workspace: saved P = 3 MFMA passes (S and O forward,
+    # dSᵀ·h from the stored P), recompute = 4 (S again in the dW kernel)
+    savep = P._lib.query("trlx_ppo_loss_from_hidden_plan", B * T, H, V, hp.lm_loss_ws.numel()) == 1
+    passes = 3 if savep else 4
+    flop = passes * 2 * nv * V * H  # over the live tokens
     ach = flop / (fused_ms * 1e-3) / 1e12
     out = {"shape": {"rows": B, "seq_len": T, "vocab": V, "hidden": H, "tokens": B * T, "live_tokens": nv,
                      "masked": masked},
@@ -467,9 +471,11 @@ def from_hidden_leg(torch, P, dev, name, steps, rounds=3):
            "rounds_ms": {k: [round(v, 4) for v in vs] for k, vs in times.items()},
            "roofline": {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "flop_per_update": flop,
-                        "note": "4 N·V·H multiply-add passes (S, O = P·W forward; S recomputed, dSᵀ·h backward) over "
-                                "the live tokens, per fused update (combine, compaction and loss tail included in "
-                                "the time)"},
+                        "mfma_passes": passes, "plan": "saved_p" if savep else "recompute",
+                        "note": "N·V·H multiply-add passes over the live tokens per fused update — saved P: S and "
+                                "O = P·W forward, dSᵀ·h from the stored bf16 P (the reference's three GEMMs' "
+                                "count); recompute: + S again in the dW kernel (combine, compaction and loss "
+                                "tail included in the time)"},
            "steps_per_round": steps, "rounds": rounds}
     del hp, h, w, ref_h, new_h
     torch.cuda.empty_cache()

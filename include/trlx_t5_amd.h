@@ -365,6 +365,9 @@ int64_t trlx_lmhead_loss_workspace_bytes(int64_t N, int64_t H, int64_t V);
  * its size as lm_workspace_bytes; a workspace of only trlx_lmhead_loss_workspace_bytes runs the
  * recompute plan. */
 int64_t trlx_ppo_loss_from_hidden_workspace_bytes(int64_t N, int64_t H, int64_t V);
+/* The plan the PPO entries run for this shape and workspace size: 1 = saved P (three MFMA
+ * passes: S and O forward, dSᵀ·h from the stored P), 0 = recompute (four: S recomputed in dW). */
+int trlx_ppo_loss_from_hidden_plan(int64_t N, int64_t H, int64_t V, int64_t lm_workspace_bytes);
 /* The smaller workspace trlx_lmhead_logprobs_bwd needs (no forward partials). */
 int64_t trlx_lmhead_loss_bwd_workspace_bytes(int64_t N, int64_t H, int64_t V);
 /* The PPO loss from the policy's last hidden states: trlx_ppo_loss_rows's arguments with the

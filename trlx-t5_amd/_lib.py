@@ -131,6 +131,7 @@ SIGNATURES = {
                                            _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
     "trlx_lmhead_loss_bwd_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64]),
     "trlx_ppo_loss_from_hidden_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64]),
+    "trlx_ppo_loss_from_hidden_plan": (_c_int, [_c_i64, _c_i64, _c_i64, _c_i64]),
     "trlx_ppo_loss_from_hidden_split": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp,
                                                  _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,
                                                  _c_f, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp,

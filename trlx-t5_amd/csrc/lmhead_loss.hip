@@ -2867,6 +2867,15 @@ extern "C" int64_t trlx_ppo_loss_from_hidden_workspace_bytes(int64_t N, int64_t 
     return int64_t(ll_carve(nullptr, N, H, V, nullptr, true, true));
 }
 
+// The saved-P plan runs when the tuning allows it and the caller's workspace holds the P tiles.
+static bool ll_savep_plan(int64_t N, int64_t H, int64_t V, int64_t lm_bytes) {
+    return (g_ll_dw == 0 || g_ll_dw == 4) && lm_bytes >= int64_t(ll_carve(nullptr, N, H, V, nullptr, true, true));
+}
+
+extern "C" int trlx_ppo_loss_from_hidden_plan(int64_t N, int64_t H, int64_t V, int64_t lm_workspace_bytes) {
+    return ll_savep_plan(N, H, V, lm_workspace_bytes) ? 1 : 0;
+}
+
 // The PPO loss side from hidden states, once `a` holds the per-token PPO fields (whitening by
 // the unsplit record or the split-beta coefficients): shapes, compaction, the three MFMA
 // launches and the combine.
@@ -2894,7 +2903,7 @@ static int ll_ppo_loss(LmLossArgs& a, const void* hidden, int64_t ldh, const voi
     TRLX_REQUIRE(lm_bytes >= int64_t(ll_carve(nullptr, N, H, V, nullptr)), TRLX_ERR_ARG,
                  "lm_workspace of %lld bytes: below trlx_lmhead_loss_workspace_bytes(%lld, %lld, %lld)",
                  (long long)lm_bytes, (long long)N, (long long)H, (long long)V);
-    const bool savep = (g_ll_dw == 0 || g_ll_dw == 4) && lm_bytes >= int64_t(ll_carve(nullptr, N, H, V, nullptr, true, true));
+    const bool savep = ll_savep_plan(N, H, V, lm_bytes);
     int rc = ll_setup(a, hidden, ldh, weight, ldw, N, H, V, labels, 1, mask, lm_workspace, dweight, dw_dtype, lddw, w,
                       s, true, savep);
     if (rc) return rc;
