@@ -1366,10 +1366,13 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     static_assert(HC % 128 == 0, "h parts of whole 128-column segments");
     static_assert(3 * kStage + 3 * kRecSlot <= 163840, "3 h stages + 3 record slots");
     static_assert(4 * (NI - 1) + 1 < DB, "every DMA piece inside the tile's gaps");
-    __shared__ __attribute__((aligned(16))) char smem[3 * kStage + 3 * kRecSlot];
+    // + each wave's RW KB of dS hand-off (below)
+    static_assert(3 * kStage + 3 * kRecSlot + 4096 * RW <= 163840, "LDS budget with the dS hand-off");
+    __shared__ __attribute__((aligned(16))) char smem[3 * kStage + 3 * kRecSlot + 4096 * RW];
     char* recs = smem + 3 * kStage;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    char* dsl = recs + 3 * kRecSlot + 1024 * RW * wave + 16 * lane;
     const int g = lane >> 4, c = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
     const int nv = a.rows ? *a.nrows : a.N;
     constexpr int vpw = 64 * RW;
@@ -1549,8 +1552,23 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
             for (int hh = 0; hh < RW; ++hh) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e)
-                    if (nb == kD + (RW * e + hh) / VPG) dsn[hh][e] = ds_of(rr[e], puse[hh][e], r0 + 16 * hh + c);
-                if (nb == kPk) dn[hh] = pack8(dsn[hh]);
+                    if (nb == kD + (RW * e + hh) / VPG) {
+                        dsn[hh][e] = ds_of(rr[e], puse[hh][e], r0 + 16 * hh + c);
+                        asm volatile("" : "+v"(dsn[hh][e]));  // formed in this gap, not sunk to the store
+                    }
+                // the next tile's A operand goes through the wave's LDS slot and is read back after
+                // this tile's last MFMA: handed over in registers (dn copied into da), hipcc gave
+                // both the same registers and sank the whole dS computation to after the last
+                // MFMA (~400 cycles a tile, serial; ISA); the store pins it to its gaps
+                if (nb == kPk) {
+                    *reinterpret_cast<bf16x8_t*>(dsl + 1024 * hh) = pack8(dsn[hh]);
+                    asm volatile("" ::: "memory");
+                }
+            }
+            if (nb == DB - 1) {
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int hh = 0; hh < RW; ++hh) dn[hh] = *reinterpret_cast<const bf16x8_t*>(dsl + 1024 * hh);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
