@@ -740,11 +740,22 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 //                                     transposed: the A operand; the lane's own 8 P values: B)
 // Software-pipelined one tile deep over a 3-stage ring (S(t+1) beside softmax(t), O(t) beside
 // nothing but tile t+2's DMA).
+#ifndef LL_FWD_PIECE_GAP
+#define LL_FWD_PIECE_GAP 4
+#endif
+#ifndef LL_FWD_PSTAGE_GAP
+#define LL_FWD_PSTAGE_GAP 13
+#endif
 template <class G, bool RESTART, bool SAVEP>
 __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit,
                                                int nv) {
     constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI, kStage = G::kStage;
     constexpr int NG = 2 * KS;  // S-phase gaps
+    // the next tile's DMA pieces every kPG-th gap of the step's S + O sequence (4: all in the S loop)
+    constexpr int kPG = LL_FWD_PIECE_GAP;
+    // SAVEP: the gap (of the S + O sequence) that stages P through LDS (after the pack at 11)
+    constexpr int kPS = LL_FWD_PSTAGE_GAP;
+    static_assert(kPS > 11 && kPS < NG + DB, "the P staging gap");
     static_assert(NG >= 20, "the P-save gaps");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -847,7 +858,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         for (int k = 0; k < NG; ++k) {
             if (k + PF < NG) af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
             s_mfma(nx, af, k);
-            if (SAVEP && k == 13) {
+            if (SAVEP && k == kPS) {
                 if (kLLAblate & 64) {  // diagnostic: no LDS round trip (wrong layout)
                     pt = __builtin_bit_cast(s16x8_t, pb);
                 } else {
@@ -867,7 +878,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                 sm_chunk(10, t, std::false_type{});
                 pb = pack8(pr);
             }
-            if ((k & 3) == 1 && (k >> 2) < NI) issue_piece(t + 2, fut, k >> 2);
+            if (k % kPG == 1 && k / kPG < NI) issue_piece(t + 2, fut, k / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
         LL_TS(ts2);
@@ -880,11 +891,12 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         for (int nb = 0; nb < DB; ++nb) {
             if (nb + PFO < DB) tf[nb + PFO] = ll16_tr_frag(cur, trb, nb + PFO);
             O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[nb], pb, O[nb], 0, 0, 0);
+            if (SAVEP && NG + nb == kPS) pt = ll_p_stage(pscr, pb, lane);
             const int gk = NG + nb;
-            if ((gk & 3) == 1 && (gk >> 2) < NI) issue_piece(t + 2, fut, gk >> 2);
+            if (gk % kPG == 1 && gk / kPG < NI) issue_piece(t + 2, fut, gk / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
-        static_assert(4 * (NI - 1) + 1 < NG, "every DMA piece before the P store (the step's counted wait)");
+        static_assert(kPG * (NI - 1) + 1 < NG + DB, "every DMA piece before the P store (the step's counted wait)");
         if (SAVEP && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);
         LL_TS(ts3);
 #if LL_STAMP
