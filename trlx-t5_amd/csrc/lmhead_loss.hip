@@ -744,7 +744,7 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 #define LL_FWD_PIECE_GAP 4
 #endif
 #ifndef LL_FWD_PSTAGE_GAP
-#define LL_FWD_PSTAGE_GAP 13
+#define LL_FWD_PSTAGE_GAP 30
 #endif
 template <class G, bool RESTART, bool SAVEP>
 __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit,
