@@ -741,7 +741,10 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 // Software-pipelined one tile deep over a 3-stage ring (S(t+1) beside softmax(t), O(t) beside
 // nothing but tile t+2's DMA).
 #ifndef LL_FWD_PIECE_GAP
-#define LL_FWD_PIECE_GAP 4
+#define LL_FWD_PIECE_GAP 2
+#endif
+#ifndef LL_FWD_PIECE_OFF
+#define LL_FWD_PIECE_OFF 1
 #endif
 #ifndef LL_FWD_PSTAGE_GAP
 #define LL_FWD_PSTAGE_GAP 30
@@ -752,7 +755,8 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI, kStage = G::kStage;
     constexpr int NG = 2 * KS;  // S-phase gaps
     // the next tile's DMA pieces every kPG-th gap of the step's S + O sequence (4: all in the S loop)
-    constexpr int kPG = LL_FWD_PIECE_GAP;
+    constexpr int kPG = LL_FWD_PIECE_GAP, kPO = LL_FWD_PIECE_OFF;
+    static_assert(kPO < kPG, "the DMA piece offset");
     // SAVEP: the gap (of the S + O sequence) that stages P through LDS (after the pack at 11)
     constexpr int kPS = LL_FWD_PSTAGE_GAP;
     static_assert(kPS > 11 && kPS < NG + DB, "the P staging gap");
@@ -878,7 +882,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                 sm_chunk(10, t, std::false_type{});
                 pb = pack8(pr);
             }
-            if (k % kPG == 1 && k / kPG < NI) issue_piece(t + 2, fut, k / kPG);
+            if (k % kPG == kPO && k / kPG < NI) issue_piece(t + 2, fut, k / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
         LL_TS(ts2);
@@ -893,10 +897,10 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[nb], pb, O[nb], 0, 0, 0);
             if (SAVEP && NG + nb == kPS) pt = ll_p_stage(pscr, pb, lane);
             const int gk = NG + nb;
-            if (gk % kPG == 1 && gk / kPG < NI) issue_piece(t + 2, fut, gk / kPG);
+            if (gk % kPG == kPO && gk / kPG < NI) issue_piece(t + 2, fut, gk / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
-        static_assert(kPG * (NI - 1) + 1 < NG + DB, "every DMA piece before the P store (the step's counted wait)");
+        static_assert(kPG * (NI - 1) + kPO < NG + DB, "every DMA piece before the P store (the step's counted wait)");
         if (SAVEP && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);
         LL_TS(ts3);
 #if LL_STAMP
@@ -1366,6 +1370,12 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
 // tile t), 3 record slots (tile t+3), P chunks in 3 register sets (tile t+3's load issued at
 // tile t), and the barrier waits only for what was issued before the previous tile (counted
 // vmcnt: P streams from HBM, 0.62 GB per call at C2).
+#ifndef LL_DWP_PIECE_GAP
+#define LL_DWP_PIECE_GAP 4
+#endif
+#ifndef LL_DWP_PIECE_OFF
+#define LL_DWP_PIECE_OFF 1
+#endif
 template <class G, int RW, int HSP>
 __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     // HSP = 2: a workgroup owns HALF the hidden columns of its vocab rows (h part hp = blockIdx
@@ -1377,7 +1387,9 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     static_assert(G::kWaves == 4, "dW: four waves per workgroup");
     static_assert(HC % 128 == 0, "h parts of whole 128-column segments");
     static_assert(3 * kStage + 3 * kRecSlot <= 163840, "3 h stages + 3 record slots");
-    static_assert(4 * (NI - 1) + 1 < DB, "every DMA piece inside the tile's gaps");
+    // the next-but-one tile's h pieces every kPG-th gap from kPO on
+    constexpr int kPG = LL_DWP_PIECE_GAP, kPO = LL_DWP_PIECE_OFF;
+    static_assert(kPO < kPG && kPG * (NI - 1) + kPO < DB, "every DMA piece inside the tile's gaps");
     // + each wave's RW KB of dS hand-off (below)
     static_assert(3 * kStage + 3 * kRecSlot + 4096 * RW <= 163840, "LDS budget with the dS hand-off");
     __shared__ __attribute__((aligned(16))) char smem[3 * kStage + 3 * kRecSlot + 4096 * RW];
@@ -1553,7 +1565,7 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
             // (the four waves' pieces in the same gaps: staggering them by wave — a wave-uniform
             // branch per gap — measured slower in both kernels, the forward's S loop 2,033 ->
             // 3,900 cycles a tile)
-            if ((nb & 3) == 1 && (nb >> 2) < NI && !(kLLAblate & 256)) issue_piece(t + 2, fut, nb >> 2, pa, pb);
+            if (nb % kPG == kPO && nb / kPG < NI && !(kLLAblate & 256)) issue_piece(t + 2, fut, nb / kPG, pa, pb);
             if (nb == 2) issue_recs(t + 3, rfut);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
