@@ -57,7 +57,7 @@ def main():
     lib.trlx_debug_ll_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     assert lib.trlx_debug_ll_stamps(buf.ctypes.data, buf.size) == 0
     out = {"config": args.config, "tune": args.tune}
-    for name, reg, cols in (("fwd", buf[:1 << 15], ["wait+barrier", "S_loop", "O_loop+store"]),
+    for name, reg, cols in (("fwd", buf[:1 << 15], ["wait+barrier", "S_loop", "O_loop+store", "of_which_exchange_barrier"]),
                             ("dw", buf[1 << 15:], ["wait+barrier", "S_phase", "dS_tail", "dW_phase"])):
         m = reg.reshape(-1, 8).astype(np.float64)
         m = m[m[:, 6] > 0]

@@ -749,6 +749,20 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 #ifndef LL_FWD_PSTAGE_GAP
 #define LL_FWD_PSTAGE_GAP 30
 #endif
+// O exchange (default): the O product splits the hidden columns over the four waves instead of
+// the tokens — wave w accumulates d blocks 16i + 4w + j (i < H/256, j < 4) for all 64 tokens of
+// the workgroup, each transposed W fragment feeding four MFMAs (one per token block) — so a wave
+// reads a quarter of the tile transposed (12 instead of 48 KB at H = 768) plus the four waves'
+// P (1 KB each, written to LDS after the softmax, read after a mid-step barrier)
+#ifndef LL_FWD_OXCH
+#define LL_FWD_OXCH 1
+#endif
+// How tile t+2 reaches LDS in step t: 0 = LDS-DMA pieces in the S loop's gaps; 1 = LDS-DMA
+// pieces in the O exchange loop's gaps; 2 = register-staged (buffer loads in the S loop's gaps,
+// ds_write_b128 in the O exchange loop's)
+#ifndef LL_FWD_FILL
+#define LL_FWD_FILL 0
+#endif
 template <class G, bool RESTART, bool SAVEP>
 __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit,
                                                int nv) {
@@ -761,11 +775,21 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     constexpr int kPS = LL_FWD_PSTAGE_GAP;
     static_assert(kPS > 11 && kPS < NG + DB, "the P staging gap");
     static_assert(NG >= 20, "the P-save gaps");
+    constexpr bool OX = LL_FWD_OXCH;
+    constexpr int OI = DB / 16, OF = 4 * OI;  // OX: the wave's 4-block d groups / its W^T fragments
+    static_assert(!OX || (DB % 16 == 0 && G::kWaves == 4 && kLLTokBlock == 64), "O exchange geometry");
+    static_assert(!OX || (kPG * (NI - 1) + kPO < NG && kPS < NG), "O exchange: the pieces and the P staging in the S loop");
+    constexpr int kFill = LL_FWD_FILL;
+    static_assert(kFill == 0 || (OX && OF == NI), "fills in the O exchange loop: one piece per gap");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // SAVEP: this wave's P transpose image (the exchange region, unused by this form) and its
     // place in the dW layout (ll_p_stage / ll_p_store)
     char* pscr = smem + 3 * kStage + wave * 4096;
+    // OX: this wave's P for the exchange (past the transpose image) and the lane's read of token
+    // block tb's (+ 4096·tb)
+    char* xch = pscr + 2048 + 16 * (lane & 63);
+    const char* xrd = smem + 3 * kStage + 2048 + 16 * (lane & 63);
     const int g = lane >> 4, c = lane & 15;
     const int split = lin / ntb, mt = lin - split * ntb;
     const int tm = mt * kLLTokBlock + wave * 16 + c;  // this lane's token (compact index)
@@ -787,14 +811,50 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
         ll16_piece(slot, i, rw, t < t1 ? off : int(0x7ffff000), lane);
     };
+    auto load_piece = [&](int t, int k) __attribute__((always_inline)) {
+        const int i = wave + G::kWaves * k;
+        const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
+        return __builtin_amdgcn_raw_buffer_load_b128(rw, ll16_piece_src(i, t < t1 ? off : int(0x7ffff000), lane), 0, 0);
+    };
     const int rb = ll16_rb(lane);
     const int trb[2] = {ll16_trb(lane, 0), ll16_trb(lane, 1)};
+    // OX: W^T fragment (i, j) = d block 16i + 4·wave + j: ll16_tr_frag's offset with the wave's
+    // part folded into the lane bases (a multiple of 256 B: the conflict-free banking unchanged)
+    const int trx[2] = {trb[0] + 8192 * (wave >> 1) + 1024 * (wave & 1), trb[1] + 8192 * (wave >> 1) + 1024 * (wave & 1)};
+    auto ox_frag = [&](const char* tile, int f) __attribute__((always_inline)) {
+        typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+        const int i = f >> 2, j = f & 3;
+        const char* base = tile + trx[j & 1] + 16384 * i + 512 * (j >> 1);
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base);
+        const s16x4_t hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + 4096));
+        const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi4.x, hi4.y, hi4.z, hi4.w};
+        return __builtin_bit_cast(bf16x8_t, v);
+    };
     float mfix = -INFINITY, mtrue = -INFINITY, lrun = 0.0f;
     if (RESTART) mfix = a.mlpart[int64_t(split) * a.N + tc].x;  // the true max pass 0 found
     bool bad = false;
-    f32x4_t O[DB];  // Oᵀ[16nb + 4g + r][token c]
+    f32x4_t O[DB];  // Oᵀ[16nb + 4g + r][token c]; OX: O[4f + tb] = Oᵀ[d block of fragment f][token block tb]
 #pragma unroll
     for (int nb = 0; nb < DB; ++nb) O[nb] = f32x4_t{};
+    // OX: O(t) over the wave's d groups for the four token blocks, after the exchange barrier
+    auto ox_product = [&](const char* tile, int gbase, auto&& gap) __attribute__((always_inline)) {
+        bf16x8_t px[4];
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb) px[tb] = *reinterpret_cast<const bf16x8_t*>(xrd + 4096 * tb);
+        constexpr int PFX = 2;
+        bf16x8_t tf[OF];
+#pragma unroll
+        for (int f = 0; f < PFX; ++f) tf[f] = ox_frag(tile, f);
+#pragma unroll
+        for (int f = 0; f < OF; ++f) {
+            if (f + PFX < OF) tf[f + PFX] = ox_frag(tile, f + PFX);
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb)
+                O[4 * f + tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[f], px[tb], O[4 * f + tb], 0, 0, 0);
+            gap(gbase + f);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
     f32x4_t s[2];  // S of the tile whose softmax comes next
     float x[8], pr[8], m4 = 0.0f, nm = 0.0f, ls = 0.0f;
     // softmax of tile t in chunks (chunk k of 12): 0 = the lane's max + the token max over its
@@ -838,14 +898,17 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     // step t (t + 1 < t1): restrict LDS regions (alias scopes, as ll_fwd_block)
     auto step = [&](const char* __restrict__ cur, const char* __restrict__ nx, char* __restrict__ fut, int t)
                     __attribute__((always_inline)) {
-        unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
+        unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts2b = 0, ts3 = 0;
         LL_TS(ts0);
         // this wave's pieces of tile t+1 (SAVEP: the previous step's P store, issued after
         // them, may still fly — it has this step to land)
-        if (SAVEP && t > t0)
+        if (kFill == 2 && t > t0) {
+            // the wave's own ds_writes of tile t+1 (the barrier's lgkmcnt); the P store may fly
+        } else if (SAVEP && t > t0) {
             __builtin_amdgcn_s_waitcnt(ll_vmcnt(1));
-        else
+        } else {
             __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));
+        }
         ll_lds_barrier();  // every wave's; every wave is done with tile t-1
         LL_TS(ts1);
         constexpr int PF = 4;
@@ -858,6 +921,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         s[1] = f32x4_t{};
         bf16x8_t pb;
         s16x8_t pt;
+        vec4u ldv[NI];  // kFill 2: tile t+2's 16-B chunks of this lane
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
             if (k + PF < NG) af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
@@ -881,11 +945,23 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             } else if (k == 11) {
                 sm_chunk(10, t, std::false_type{});
                 pb = pack8(pr);
+            } else if (OX && k == 12) {
+                *reinterpret_cast<bf16x8_t*>(xch) = pb;  // the exchange: read after the S loop's barrier
             }
-            if (k % kPG == kPO && k / kPG < NI) issue_piece(t + 2, fut, k / kPG);
+            if (kFill == 0 && k % kPG == kPO && k / kPG < NI && !(kLLAblate & 2048)) issue_piece(t + 2, fut, k / kPG);
+            if (kFill == 2 && k % kPG == kPO && k / kPG < NI) ldv[k / kPG] = load_piece(t + 2, k / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
         LL_TS(ts2);
+        if constexpr (OX) {
+            ll_lds_barrier();  // every wave's P(t) in the exchange
+            LL_TS(ts2b);
+            ox_product(cur, NG, [&](int gk) __attribute__((always_inline)) {
+                const int f = gk - NG;
+                if (kFill == 1 && !(kLLAblate & 2048)) issue_piece(t + 2, fut, f);
+                if (kFill == 2) *reinterpret_cast<vec4u*>(fut + (wave + G::kWaves * f) * 1024 + 16 * lane) = ldv[f];
+            });
+        } else {
         // ---- O(t): tr reads of tile t's W (cur) | MFMA
         constexpr int PFO = 4;
         bf16x8_t tf[DB];
@@ -900,6 +976,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             if (gk % kPG == kPO && gk / kPG < NI) issue_piece(t + 2, fut, gk / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
+        }
         static_assert(kPG * (NI - 1) + kPO < NG + DB, "every DMA piece before the P store (the step's counted wait)");
         if (SAVEP && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);
         LL_TS(ts3);
@@ -907,9 +984,10 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         stamp[0] += ts1 - ts0;
         stamp[1] += ts2 - ts1;
         stamp[2] += ts3 - ts2;
+        if (OX) stamp[3] += ts2b - ts2;
         stamp[6] += 1;
 #endif
-        (void)ts0, (void)ts1, (void)ts2, (void)ts3;
+        (void)ts0, (void)ts1, (void)ts2, (void)ts2b, (void)ts3;
     };
     if (t0 < t1) {
         char* c0 = smem;
@@ -939,9 +1017,16 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
 #pragma unroll
         for (int k = 0; k < 11; ++k) sm_chunk(k, t1 - 1, std::true_type{});
         const bf16x8_t pb = pack8(pr);
+        if constexpr (OX) {
+            ll_lds_barrier();  // every wave is done reading the exchange of the previous tile
+            *reinterpret_cast<bf16x8_t*>(xch) = pb;
+            ll_lds_barrier();
+            ox_product(c0, 0, [](int) {});
+        } else {
 #pragma unroll
-        for (int nb = 0; nb < DB; ++nb)
-            O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ll16_tr_frag(c0, trb, nb), pb, O[nb], 0, 0, 0);
+            for (int nb = 0; nb < DB; ++nb)
+                O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ll16_tr_frag(c0, trb, nb), pb, O[nb], 0, 0, 0);
+        }
         if (SAVEP) ll_p_store(a, ll_p_stage(pscr, pb, lane), t1 - 1, ptt, phalf, lane);
     }
 #if LL_STAMP
@@ -959,7 +1044,20 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     const float mrun = any ? mt4 : mfix;
     float lt = lrun + __shfl_xor(lrun, 16);
     lt = lt + __shfl_xor(lt, 32);
-    if (valid) {
+    if constexpr (OX) {
+        // Oᵀ of token block tb, d = 16(16i + 4·wave + j) + 4g + r
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb) {
+            const int tmb = mt * kLLTokBlock + 16 * tb + c;
+            if (tmb < nv) {
+                float* op = a.opart + (int64_t(split) * a.N + tmb) * a.H + 64 * wave + 4 * g;
+#pragma unroll
+                for (int f = 0; f < OF; ++f)
+                    *reinterpret_cast<f32x4_t*>(op + 256 * (f >> 2) + 16 * (f & 3)) = O[4 * f + tb];
+            }
+        }
+        if (valid && g == 0) a.mlpart[int64_t(split) * a.N + tm] = make_float2(mrun, lt);
+    } else if (valid) {
         float* op = a.opart + (int64_t(split) * a.N + tm) * a.H + 4 * g;
 #pragma unroll
         for (int nb = 0; nb < DB; ++nb) *reinterpret_cast<f32x4_t*>(op + 16 * nb) = O[nb];
