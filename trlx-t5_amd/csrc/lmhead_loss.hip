@@ -255,6 +255,19 @@ __device__ __forceinline__ float ll_pair_max(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// max / sum over the four 16-lane rows (lanes l, l^16, l^32, l^48: one token's four lane groups
+// in the 16x16x32 forms), the same bits in every lane.  v_permlane16/32_swap are VALU: a
+// __shfl_xor is a ds_bpermute, an LDS round trip whose lgkmcnt(0) also drains the operand reads
+// in flight.
+__device__ __forceinline__ float ll_rows_max(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return ll_pair_max(fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
+}
+__device__ __forceinline__ float ll_pair_sum(float v);
+__device__ __forceinline__ float ll_rows_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return ll_pair_sum(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+}
 __device__ __forceinline__ float ll_pair_sum(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -870,8 +883,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             }
             const float lm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])),
                                    fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
-            m4 = fmaxf(lm, __shfl_xor(lm, 16));
-            m4 = fmaxf(m4, __shfl_xor(m4, 32));
+            m4 = ll_rows_max(lm);
         } else if (k == 1) {
             if (!RESTART) {
                 mtrue = fmaxf(mtrue, m4);
@@ -936,8 +948,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             if (k == 0) {  // the lane's max + token max (no mask inside the loop: see ll_fwd_block)
                 const float lm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])),
                                        fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
-                m4 = fmaxf(lm, __shfl_xor(lm, 16));
-                m4 = fmaxf(m4, __shfl_xor(m4, 32));
+                m4 = ll_rows_max(lm);
             } else if (k == 2) {
                 sm_chunk(1, t, std::false_type{});
             } else if (k >= 3 && k < 11) {
@@ -1039,11 +1050,9 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         any = __any(bad);
         if (lane == 0) a.flags[lin * G::kWaves + wave] = any;
     }
-    float mt4 = fmaxf(mtrue, __shfl_xor(mtrue, 16));
-    mt4 = fmaxf(mt4, __shfl_xor(mt4, 32));
+    const float mt4 = ll_rows_max(mtrue);
     const float mrun = any ? mt4 : mfix;
-    float lt = lrun + __shfl_xor(lrun, 16);
-    lt = lt + __shfl_xor(lt, 32);
+    const float lt = ll_rows_sum(lrun);
     if constexpr (OX) {
         // Oᵀ of token block tb, d = 16(16i + 4·wave + j) + 4g + r
 #pragma unroll
