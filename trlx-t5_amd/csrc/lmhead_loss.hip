@@ -773,6 +773,9 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 // How tile t+2 reaches LDS in step t: 0 = LDS-DMA pieces in the S loop's gaps; 1 = LDS-DMA
 // pieces in the O exchange loop's gaps; 2 = register-staged (buffer loads in the S loop's gaps,
 // ds_write_b128 in the O exchange loop's)
+#ifndef LL_FWD_PF
+#define LL_FWD_PF 4
+#endif
 #ifndef LL_FWD_FILL
 #define LL_FWD_FILL 0
 #endif
@@ -923,7 +926,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         }
         ll_lds_barrier();  // every wave's; every wave is done with tile t-1
         LL_TS(ts1);
-        constexpr int PF = 4;
+        constexpr int PF = LL_FWD_PF;  // W row fragments in flight (LDS latency under a saturated array)
         bf16x8_t af[NG];
 #pragma unroll
         for (int k = 0; k < PF; ++k) af[k] = ll16_row_frag(nx, rb, k / KS, k % KS);
