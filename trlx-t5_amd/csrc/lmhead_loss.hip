@@ -853,14 +853,13 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
 #pragma unroll
     for (int nb = 0; nb < DB; ++nb) O[nb] = f32x4_t{};
     // OX: O(t) over the wave's d groups for the four token blocks, after the exchange barrier
-    auto ox_product = [&](const char* tile, int gbase, auto&& gap) __attribute__((always_inline)) {
+    // (the first PFX fragments come in tf: read before the exchange barrier, they depend on the
+    // tile only)
+    constexpr int PFX = 2;
+    auto ox_product = [&](const char* tile, bf16x8_t (&tf)[OF], int gbase, auto&& gap) __attribute__((always_inline)) {
         bf16x8_t px[4];
 #pragma unroll
         for (int tb = 0; tb < 4; ++tb) px[tb] = *reinterpret_cast<const bf16x8_t*>(xrd + 4096 * tb);
-        constexpr int PFX = 2;
-        bf16x8_t tf[OF];
-#pragma unroll
-        for (int f = 0; f < PFX; ++f) tf[f] = ox_frag(tile, f);
 #pragma unroll
         for (int f = 0; f < OF; ++f) {
             if (f + PFX < OF) tf[f + PFX] = ox_frag(tile, f + PFX);
@@ -937,6 +936,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         bf16x8_t pb;
         s16x8_t pt;
         vec4u ldv[NI];  // kFill 2: tile t+2's 16-B chunks of this lane
+        bf16x8_t tfx[OF];  // OX: tile t's transposed fragments (the first PFX in the S loop's last gaps)
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
             if (k + PF < NG) af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
@@ -964,13 +964,14 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             }
             if (kFill == 0 && k % kPG == kPO && k / kPG < NI && !(kLLAblate & 2048)) issue_piece(t + 2, fut, k / kPG);
             if (kFill == 2 && k % kPG == kPO && k / kPG < NI) ldv[k / kPG] = load_piece(t + 2, k / kPG);
+            if (OX && k >= NG - PFX) tfx[k - (NG - PFX)] = ox_frag(cur, k - (NG - PFX));
             __builtin_amdgcn_sched_barrier(0);
         }
         LL_TS(ts2);
         if constexpr (OX) {
             ll_lds_barrier();  // every wave's P(t) in the exchange
             LL_TS(ts2b);
-            ox_product(cur, NG, [&](int gk) __attribute__((always_inline)) {
+            ox_product(cur, tfx, NG, [&](int gk) __attribute__((always_inline)) {
                 const int f = gk - NG;
                 if (kFill == 1 && !(kLLAblate & 2048)) issue_piece(t + 2, fut, f);
                 if (kFill == 2) *reinterpret_cast<vec4u*>(fut + (wave + G::kWaves * f) * 1024 + 16 * lane) = ldv[f];
@@ -1035,7 +1036,10 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             ll_lds_barrier();  // every wave is done reading the exchange of the previous tile
             *reinterpret_cast<bf16x8_t*>(xch) = pb;
             ll_lds_barrier();
-            ox_product(c0, 0, [](int) {});
+            bf16x8_t tfx[OF];
+#pragma unroll
+            for (int f = 0; f < PFX; ++f) tfx[f] = ox_frag(c0, f);
+            ox_product(c0, tfx, 0, [](int) {});
         } else {
 #pragma unroll
             for (int nb = 0; nb < DB; ++nb)
