@@ -597,3 +597,33 @@ def test_hot_path_h_sliced_matches_row_split(B, T, V, H, masked):
         torch.testing.assert_close(b[5], a[5], rtol=1e-5, atol=1e-5)
         assert _rel(b[2], a[2]) < 4e-3 and _rel(b[3], a[3]) < 4e-3
         assert torch.isfinite(b[2]).all() and torch.isfinite(b[3]).all()
+
+
+def test_lm_head_logprobs_autograd_no_device_allocation_in_steady_state():
+    """The drop-in autograd path takes its lp / lse / E / workspace / dh / dW buffers per call
+    from PyTorch's stream-ordered caching allocator (lm_head.py): after the first step no call
+    reaches hipMalloc — the segment count and the reserved bytes stay put — so a per-call
+    torch.empty costs a free-list pop, and two streams never share a workspace (a workspace
+    cached in the module would)."""
+    N, H, V = 1024, 768, 50257
+    h, w, y = _operands(N, H, V, seed=11)
+    h = h.to(DEV).requires_grad_(True)
+    w = w.to(DEV).requires_grad_(True)
+    y = y.to(DEV)
+
+    def step():
+        lp = P.lm_head_logprobs(h, w, y)
+        lp.float().sum().backward()
+        h.grad = None
+        w.grad = None
+
+    step()
+    step()
+    torch.cuda.synchronize()
+    st0 = torch.cuda.memory_stats(DEV)
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    st1 = torch.cuda.memory_stats(DEV)
+    assert st1["segment.all.allocated"] == st0["segment.all.allocated"]
+    assert st1["reserved_bytes.all.current"] == st0["reserved_bytes.all.current"]
