@@ -776,6 +776,14 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 #ifndef LL_FWD_PF
 #define LL_FWD_PF 4
 #endif
+// S split over the hidden halves of a wave pair (needs the O exchange): wave w = (hidden half
+// w & 1, token pair w >> 1) accumulates partial S over its half for BOTH token blocks of the
+// pair (h fragments: 2 blocks x H/2 = the same 96 registers), so each W row fragment feeds two
+// MFMAs and a wave reads half the tile by rows; the partner's partial of the wave's own block
+// comes through LDS (written in the O loop, read after the next step's barrier)
+#ifndef LL_FWD_SPAIR
+#define LL_FWD_SPAIR 1
+#endif
 #ifndef LL_FWD_FILL
 #define LL_FWD_FILL 0
 #endif
@@ -797,6 +805,9 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     static_assert(!OX || (kPG * (NI - 1) + kPO < NG && kPS < NG), "O exchange: the pieces and the P staging in the S loop");
     constexpr int kFill = LL_FWD_FILL;
     static_assert(kFill == 0 || (OX && OF == NI), "fills in the O exchange loop: one piece per gap");
+    constexpr bool SP = LL_FWD_SPAIR;
+    constexpr int KH = KS / 2;  // SP: k-steps of a hidden half
+    static_assert(!SP || (OX && KH % 4 == 0 && kFill == 0), "S pair split: the O exchange, whole 128-column segments");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // SAVEP: this wave's P transpose image (the exchange region, unused by this form) and its
@@ -813,12 +824,29 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     const bool valid = tm < nv;
     const int tc = valid ? tm : nv - 1;
     const int row = a.rows ? a.rows[tc] : tc;
-    bf16x8_t hf[KS];  // B operand of S: lane (g, c) -> h[token c][32ks + 8g .. +7]
-    {
+    // B operand of S: lane (g, c) -> h[token c][32ks + 8g .. +7]; SP: hf[ks] own token block,
+    // hf[KH + ks] the partner's (wave ^ 1), columns (H/2)(wave & 1) + 32ks + 8g
+    bf16x8_t hf[KS];
+    if constexpr (SP) {
+        const int tmp = mt * kLLTokBlock + (wave ^ 1) * 16 + c;
+        const int tcp = tmp < nv ? tmp : nv - 1;
+        const int rowp = a.rows ? a.rows[tcp] : tcp;
+        const uint16_t* hp = a.h + int64_t(row) * a.ldh + (H / 2) * (wave & 1) + 8 * g;
+        const uint16_t* hq = a.h + int64_t(rowp) * a.ldh + (H / 2) * (wave & 1) + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KH; ++ks) {
+            hf[ks] = *reinterpret_cast<const bf16x8_t*>(hp + 32 * ks);
+            hf[KH + ks] = *reinterpret_cast<const bf16x8_t*>(hq + 32 * ks);
+        }
+    } else {
         const uint16_t* hp = a.h + int64_t(row) * a.ldh + 8 * g;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) hf[ks] = *reinterpret_cast<const bf16x8_t*>(hp + 32 * ks);
     }
+    // SP: this wave's half of the W rows (rb + the half's segments) and the partner's partial S
+    const int rbh = ll16_rb(lane) + KS * 1024 * (wave & 1);
+    const char* sxr = smem + 3 * kStage + (wave ^ 1) * 4096 + 16 * (lane & 63);
+    char* sxw = pscr + 16 * (lane & 63);
     const int nvt = (a.V + kLLRows - 1) / kLLRows;
     const int t0 = int(int64_t(split) * nvt / nsplit), t1 = int(int64_t(split + 1) * nvt / nsplit);
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
@@ -870,7 +898,8 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    f32x4_t s[2];  // S of the tile whose softmax comes next
+    f32x4_t s[2];  // S of the tile whose softmax comes next (SP: the wave's partial of its own block)
+    f32x4_t so[2];  // SP: the partial of the partner's block (to the exchange)
     float x[8], pr[8], m4 = 0.0f, nm = 0.0f, ls = 0.0f;
     // softmax of tile t in chunks (chunk k of 12): 0 = the lane's max + the token max over its
     // four lanes, 1 = offset / overflow flag, 2..9 = one exp each, 10 = the row sum
@@ -903,8 +932,24 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         }
     };
     auto s_mfma = [&](const char* tile, bf16x8_t* af, int k) __attribute__((always_inline)) {
-        const int mb = k / KS, ks = k % KS;
-        s[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], hf[ks], s[mb], 0, 0, 0);
+        if constexpr (SP) {  // gap k: fragment k/2 = (k-step k/4, block (k/2)&1), token block k&1
+            const int fa = k >> 1, mb = fa & 1, ks = fa >> 1;
+            if (k & 1)
+                so[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fa], hf[KH + ks], so[mb], 0, 0, 0);
+            else
+                s[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fa], hf[ks], s[mb], 0, 0, 0);
+        } else {
+            const int mb = k / KS, ks = k % KS;
+            s[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k], hf[ks], s[mb], 0, 0, 0);
+        }
+    };
+    // SP: W row fragment fa of a tile (rows 16(fa&1) + c, the half's k-step fa>>1)
+    auto sp_frag = [&](const char* tile, int fa) __attribute__((always_inline)) {
+        return ll16_row_frag(tile, rbh, fa & 1, fa >> 1);
+    };
+    auto sx_write = [&]() __attribute__((always_inline)) {
+        *reinterpret_cast<f32x4_t*>(sxw) = so[0];
+        *reinterpret_cast<f32x4_t*>(sxw + 1024) = so[1];
     };
 #if LL_STAMP
     unsigned long long stamp[8] = {};
@@ -927,21 +972,36 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         LL_TS(ts1);
         constexpr int PF = LL_FWD_PF;  // W row fragments in flight (LDS latency under a saturated array)
         bf16x8_t af[NG];
+        f32x4_t xr[2];
+        if constexpr (SP) {
+            xr[0] = *reinterpret_cast<const f32x4_t*>(sxr);  // the partner's partial of S(t)
+            xr[1] = *reinterpret_cast<const f32x4_t*>(sxr + 1024);
 #pragma unroll
-        for (int k = 0; k < PF; ++k) af[k] = ll16_row_frag(nx, rb, k / KS, k % KS);
+            for (int k = 0; k < PF; ++k) af[k] = sp_frag(nx, k);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = s[e >> 2][e & 3];  // S(t) for the softmax; S(t+1) accumulates anew
+            for (int k = 0; k < PF; ++k) af[k] = ll16_row_frag(nx, rb, k / KS, k % KS);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e)  // S(t) for the softmax; S(t+1) accumulates anew
+            x[e] = SP ? s[e >> 2][e & 3] + xr[e >> 2][e & 3] : s[e >> 2][e & 3];
         s[0] = f32x4_t{};
         s[1] = f32x4_t{};
+        so[0] = f32x4_t{};
+        so[1] = f32x4_t{};
         bf16x8_t pb;
         s16x8_t pt;
         vec4u ldv[NI];  // kFill 2: tile t+2's 16-B chunks of this lane
         bf16x8_t tfx[OF];  // OX: tile t's transposed fragments (the first PFX in the S loop's last gaps)
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
-            if (k + PF < NG) af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
+            if (SP) {
+                if (!(k & 1) && (k >> 1) + PF < KS) af[(k >> 1) + PF] = sp_frag(nx, (k >> 1) + PF);
+            } else if (k + PF < NG) {
+                af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
+            }
             s_mfma(nx, af, k);
-            if (SAVEP && k == kPS) {
+            if (SAVEP && !SP && k == kPS) {
                 if (kLLAblate & 64) {  // diagnostic: no LDS round trip (wrong layout)
                     pt = __builtin_bit_cast(s16x8_t, pb);
                 } else {
@@ -973,6 +1033,10 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             LL_TS(ts2b);
             ox_product(cur, tfx, NG, [&](int gk) __attribute__((always_inline)) {
                 const int f = gk - NG;
+                // SP: P(t) through the transpose image, then S(t+1)'s partner partial into the
+                // same region (the partner read the last one before the exchange barrier)
+                if (SP && SAVEP && f == 0) pt = ll_p_stage(pscr, pb, lane);
+                if (SP && f == 1) sx_write();
                 if (kFill == 1 && !(kLLAblate & 2048)) issue_piece(t + 2, fut, f);
                 if (kFill == 2) *reinterpret_cast<vec4u*>(fut + (wave + G::kWaves * f) * 1024 + 16 * lane) = ldv[f];
             });
@@ -1016,10 +1080,22 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         ll_lds_barrier();
         s[0] = f32x4_t{};
         s[1] = f32x4_t{};
+        if constexpr (SP) {
+            so[0] = f32x4_t{};
+            so[1] = f32x4_t{};
 #pragma unroll
-        for (int k = 0; k < NG; ++k) {
-            const bf16x8_t af = ll16_row_frag(c0, rb, k / KS, k % KS);
-            s[k / KS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, hf[k % KS], s[k / KS], 0, 0, 0);
+            for (int fa = 0; fa < KS; ++fa) {
+                const bf16x8_t f = sp_frag(c0, fa);
+                s[fa & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, hf[fa >> 1], s[fa & 1], 0, 0, 0);
+                so[fa & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, hf[KH + (fa >> 1)], so[fa & 1], 0, 0, 0);
+            }
+            sx_write();
+        } else {
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                const bf16x8_t af = ll16_row_frag(c0, rb, k / KS, k % KS);
+                s[k / KS] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, hf[k % KS], s[k / KS], 0, 0, 0);
+            }
         }
         for (int t = t0; t + 1 < t1; ++t) {
             step(c0, c1, c2, t);
@@ -1029,11 +1105,16 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             c2 = cc;
         }
         // the last tile: its (masked) softmax and O product
+        if constexpr (SP) {
+            ll_lds_barrier();  // the partner's partial of the last tile; every wave done with the P exchange
+            s[0] += *reinterpret_cast<const f32x4_t*>(sxr);
+            s[1] += *reinterpret_cast<const f32x4_t*>(sxr + 1024);
+        }
 #pragma unroll
         for (int k = 0; k < 11; ++k) sm_chunk(k, t1 - 1, std::true_type{});
         const bf16x8_t pb = pack8(pr);
         if constexpr (OX) {
-            ll_lds_barrier();  // every wave is done reading the exchange of the previous tile
+            if (!SP) ll_lds_barrier();  // every wave is done reading the exchange of the previous tile
             *reinterpret_cast<bf16x8_t*>(xch) = pb;
             ll_lds_barrier();
             bf16x8_t tfx[OF];
