@@ -794,7 +794,9 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     constexpr int NG = 2 * KS;  // S-phase gaps
     // the next tile's DMA pieces every kPG-th gap of the step's S + O sequence (4: all in the S loop)
     constexpr int kPG = LL_FWD_PIECE_GAP, kPO = LL_FWD_PIECE_OFF;
-    static_assert(kPO < kPG, "the DMA piece offset");
+    static_assert(kPO >= 0, "the DMA piece offset (the first piece's gap)");
+    // piece i of tile t+2 in gap kPO + kPG·i
+    auto piece_at = [](int k) { return k >= kPO && (k - kPO) % kPG == 0 && (k - kPO) / kPG < NI; };
     // SAVEP: the gap (of the S + O sequence) that stages P through LDS (after the pack at 11)
     constexpr int kPS = LL_FWD_PSTAGE_GAP;
     static_assert(kPS > 11 && kPS < NG + DB, "the P staging gap");
@@ -1022,8 +1024,8 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             } else if (OX && k == 12) {
                 *reinterpret_cast<bf16x8_t*>(xch) = pb;  // the exchange: read after the S loop's barrier
             }
-            if (kFill == 0 && k % kPG == kPO && k / kPG < NI && !(kLLAblate & 2048)) issue_piece(t + 2, fut, k / kPG);
-            if (kFill == 2 && k % kPG == kPO && k / kPG < NI) ldv[k / kPG] = load_piece(t + 2, k / kPG);
+            if (kFill == 0 && piece_at(k) && !(kLLAblate & 2048)) issue_piece(t + 2, fut, (k - kPO) / kPG);
+            if (kFill == 2 && piece_at(k)) ldv[(k - kPO) / kPG] = load_piece(t + 2, (k - kPO) / kPG);
             if (OX && k >= NG - PFX) tfx[k - (NG - PFX)] = ox_frag(cur, k - (NG - PFX));
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -1052,7 +1054,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[nb], pb, O[nb], 0, 0, 0);
             if (SAVEP && NG + nb == kPS) pt = ll_p_stage(pscr, pb, lane);
             const int gk = NG + nb;
-            if (gk % kPG == kPO && gk / kPG < NI) issue_piece(t + 2, fut, gk / kPG);
+            if (piece_at(gk)) issue_piece(t + 2, fut, (gk - kPO) / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
         }
