@@ -1567,6 +1567,9 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
 // tile t), 3 record slots (tile t+3), P chunks in 3 register sets (tile t+3's load issued at
 // tile t), and the barrier waits only for what was issued before the previous tile (counted
 // vmcnt: P streams from HBM, 0.62 GB per call at C2).
+#ifndef LL_DWP_PFO
+#define LL_DWP_PFO 8  // transposed h fragments in flight
+#endif
 #ifndef LL_DWP_PIECE_GAP
 #define LL_DWP_PIECE_GAP 4
 #endif
@@ -1746,7 +1749,7 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
         // ≈ 128 MFMA cycles later; one at a time, so the VALU work hides behind the MFMAs of
         // its gap: four values in one gap had cost ~400 cycles a tile), the packs after them;
         // transposed reads PFO fragments ahead (≈ 256 MFMA cycles)
-        constexpr int PFO = 8, L = 8 / RW, kR = 1, kD = kR + 1 + L;
+        constexpr int PFO = LL_DWP_PFO, L = 8 / RW, kR = 1, kD = kR + 1 + L;
         constexpr int VPG = (8 * RW + (DB - kD - 2)) / (DB - kD - 1);  // dS values per gap
         constexpr int kPk = kD + (8 * RW + VPG - 1) / VPG;
         static_assert(kPk < DB, "the dS gaps");
