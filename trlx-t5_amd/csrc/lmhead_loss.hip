@@ -741,9 +741,10 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 }
 
 // ------------------------------------------------------------------ forward, 16x16x32 form
-// One wave per 16 tokens over the WHOLE hidden dimension (h fragments 96 registers, O 192 at
-// H = 768), the k_lmloss_dw layout with the roles swapped, so no partial S crosses waves and a
-// step has one barrier.  Per 32-row W tile, on v_mfma_f32_16x16x32_bf16:
+// A workgroup = 64 tokens (four blocks of 16, one softmax per wave: block w) x one vocab split;
+// h fragments 96 registers, O 192 at H = 768.  Without the two splits below (LL_FWD_SPAIR,
+// LL_FWD_OXCH — both on by default) a wave computes S and O of its own block over the whole H,
+// the k_lmloss_dw layout with the roles swapped.  Per 32-row W tile, on v_mfma_f32_16x16x32_bf16:
 //   S[v][t] = Σ_d W[v][d]·h[t][d]     2 vocab blocks x H/32 k-steps (W rows the A operand, the
 //                                     h fragments the B operand): lane (g, c) ends with vocab
 //                                     rows 16mb + 4g + r of token c
@@ -751,8 +752,8 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 //                                     max over its 4 lanes (g), fixed for the split, as ll_fwd_block
 //   Oᵀ[d][t] += Σ_v W[v][d]·P[v][t]   H/16 column blocks x one permuted k-step (W read
 //                                     transposed: the A operand; the lane's own 8 P values: B)
-// Software-pipelined one tile deep over a 3-stage ring (S(t+1) beside softmax(t), O(t) beside
-// nothing but tile t+2's DMA).
+// Software-pipelined one tile deep over a 3-stage ring: S(t+1) beside softmax(t) and tile t+2's
+// DMA, one barrier, O(t) (DESIGN.md §3 "The forward at HEAD").
 #ifndef LL_FWD_PIECE_GAP
 #define LL_FWD_PIECE_GAP 2
 #endif
@@ -770,9 +771,7 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 #ifndef LL_FWD_OXCH
 #define LL_FWD_OXCH 1
 #endif
-// How tile t+2 reaches LDS in step t: 0 = LDS-DMA pieces in the S loop's gaps; 1 = LDS-DMA
-// pieces in the O exchange loop's gaps; 2 = register-staged (buffer loads in the S loop's gaps,
-// ds_write_b128 in the O exchange loop's)
+// W row fragments in flight in the S loop
 #ifndef LL_FWD_PF
 #define LL_FWD_PF 4
 #endif
@@ -784,6 +783,9 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 #ifndef LL_FWD_SPAIR
 #define LL_FWD_SPAIR 1
 #endif
+// How tile t+2 reaches LDS in step t: 0 = LDS-DMA pieces in the S loop's gaps; 1 = LDS-DMA
+// pieces in the O exchange loop's gaps; 2 = register-staged (buffer loads in the S loop's gaps,
+// ds_write_b128 in the O exchange loop's) — 1 and 2 measured slower (profiles/r05f_fwd_oxch.txt)
 #ifndef LL_FWD_FILL
 #define LL_FWD_FILL 0
 #endif
@@ -792,12 +794,13 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                                                int nv) {
     constexpr int H = G::H, KS = H / 32, DB = H / 16, NI = G::NI, kStage = G::kStage;
     constexpr int NG = 2 * KS;  // S-phase gaps
-    // the next tile's DMA pieces every kPG-th gap of the step's S + O sequence (4: all in the S loop)
+    // tile t+2's DMA pieces: every kPG-th gap of the step's S + O sequence from gap kPO
     constexpr int kPG = LL_FWD_PIECE_GAP, kPO = LL_FWD_PIECE_OFF;
     static_assert(kPO >= 0, "the DMA piece offset (the first piece's gap)");
     // piece i of tile t+2 in gap kPO + kPG·i
     auto piece_at = [](int k) { return k >= kPO && (k - kPO) % kPG == 0 && (k - kPO) / kPG < NI; };
-    // SAVEP: the gap (of the S + O sequence) that stages P through LDS (after the pack at 11)
+    // SAVEP: the gap (of the S + O sequence) that stages P through LDS (after the pack at 11;
+    // with LL_FWD_SPAIR the O loop's first gap instead)
     constexpr int kPS = LL_FWD_PSTAGE_GAP;
     static_assert(kPS > 11 && kPS < NG + DB, "the P staging gap");
     static_assert(NG >= 20, "the P-save gaps");
