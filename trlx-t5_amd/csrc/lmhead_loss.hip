@@ -443,6 +443,18 @@ __device__ __forceinline__ s16x8_t ll_p_stage(char* pscr, bf16x8_t pb, int lane)
     const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(rd + 4 * kLLPRow));
     return s16x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 }
+// The same transpose read straight from the wave's O-exchange slot (the 16 B of P a lane wrote
+// at slot + 16·lane, LL_FWD_OXCH): the 8-B chunk (token R, lane group g', block mb) that the image
+// above holds at kLLPRow·R + 8g' + 32mb sits at 16·(16g' + R) + 8mb, so the two tr reads take
+// those addresses and no image is written (4-way bank conflicts on 2 reads a tile instead).
+__device__ __forceinline__ s16x8_t ll_p_stage_slot(const char* slot, int lane) {
+    typedef __attribute__((address_space(3))) s16x4_t lds_s4;
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const char* rd = slot + 16 * (16 * p + 8 * (g & 1) + q) + 8 * (g >> 1);
+    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)rd);
+    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(rd + 64));
+    return s16x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+}
 __device__ __forceinline__ void ll_p_store(const LmLossArgs& a, const s16x8_t& v, int t, int tt, int half,
                                            int lane) {
     const int g = lane >> 4, c = lane & 15;
@@ -789,6 +801,10 @@ __device__ __forceinline__ void ll_fwd_block(const LmLossArgs& a, char* smem, in
 #ifndef LL_FWD_FILL
 #define LL_FWD_FILL 0
 #endif
+// SAVEP with the O exchange: the saved-P transpose read from the exchange slot (ll_p_stage_slot)
+#ifndef LL_FWD_PSLOT
+#define LL_FWD_PSLOT 1
+#endif
 template <class G, bool RESTART, bool SAVEP>
 __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, int lin, int ntb, int nsplit,
                                                int nv) {
@@ -822,6 +838,14 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     // block tb's (+ 4096·tb)
     char* xch = pscr + 2048 + 16 * (lane & 63);
     const char* xrd = smem + 3 * kStage + 2048 + 16 * (lane & 63);
+    constexpr bool PSL = OX && LL_FWD_PSLOT;  // the saved-P transpose from the exchange slot
+    static_assert(!PSL || kPS > 12, "the saved-P transpose after the exchange slot's write (gap 12)");
+    auto p_stage = [&](const bf16x8_t& pbv) __attribute__((always_inline)) {
+        if constexpr (PSL)
+            return ll_p_stage_slot(pscr + 2048, lane);
+        else
+            return ll_p_stage(pscr, pbv, lane);
+    };
     const int g = lane >> 4, c = lane & 15;
     const int split = lin / ntb, mt = lin - split * ntb;
     const int tm = mt * kLLTokBlock + wave * 16 + c;  // this lane's token (compact index)
@@ -1006,11 +1030,11 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                 af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
             }
             s_mfma(nx, af, k);
-            if (SAVEP && !SP && k == kPS) {
+            if (SAVEP && (!SP || PSL) && k == kPS) {
                 if (kLLAblate & 64) {  // diagnostic: no LDS round trip (wrong layout)
                     pt = __builtin_bit_cast(s16x8_t, pb);
                 } else {
-                    pt = ll_p_stage(pscr, pb, lane);
+                    pt = p_stage(pb);  // PSL: after the slot write at gap 12
                 }
             }
             if (k == 0) {  // the lane's max + token max (no mask inside the loop: see ll_fwd_block)
@@ -1040,7 +1064,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                 const int f = gk - NG;
                 // SP: P(t) through the transpose image, then S(t+1)'s partner partial into the
                 // same region (the partner read the last one before the exchange barrier)
-                if (SP && SAVEP && f == 0) pt = ll_p_stage(pscr, pb, lane);
+                if (SP && SAVEP && !PSL && f == 0) pt = ll_p_stage(pscr, pb, lane);
                 if (SP && f == 1) sx_write();
                 if (kFill == 1 && !(kLLAblate & 2048)) issue_piece(t + 2, fut, f);
                 if (kFill == 2) *reinterpret_cast<vec4u*>(fut + (wave + G::kWaves * f) * 1024 + 16 * lane) = ldv[f];
@@ -1131,7 +1155,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             for (int nb = 0; nb < DB; ++nb)
                 O[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ll16_tr_frag(c0, trb, nb), pb, O[nb], 0, 0, 0);
         }
-        if (SAVEP) ll_p_store(a, ll_p_stage(pscr, pb, lane), t1 - 1, ptt, phalf, lane);
+        if (SAVEP) ll_p_store(a, p_stage(pb), t1 - 1, ptt, phalf, lane);
     }
 #if LL_STAMP
     if (!RESTART && lane == 0 && lin * 4 + wave < (1 << 12))
