@@ -412,12 +412,24 @@ FROM_HIDDEN_SHAPES = {  # name: (rows, T, V, H, masked) — BASELINE configs[1] 
 
 def from_hidden_leg(torch, P, dev, name, steps, rounds=3):
     """§8f-2, loss side, as the driver runs it: the PPO update from the policy's hidden states
-    (PPOHotPath.policy_loss_from_hidden after one experience_from_hidden), the fused MFMA route
-    (csrc/lmhead_loss.hip: no [N, V] logits / dlogits in HBM) against the reference's structure on
-    the hot path's kernels (route "gemm": hipBLASLt bf16 logits -> fused loss rows -> hipBLASLt
-    dh and dW GEMMs), `steps` updates per route per round, rounds interleaved (the first route
-    alternates), HIP events on the launch stream around each round; the deferred loss tail of
-    every update runs inside the timed region.  Per-update times are the median over rounds."""
+    after one experience_from_hidden, `steps` updates per route per round, rounds interleaved
+    (the first route rotates), HIP events on the launch stream around each round; the deferred
+    loss tail of every hot-path update runs inside the timed region.  Per-update times are the
+    median over rounds.  Routes:
+      fused         PPOHotPath.policy_loss_from_hidden (csrc/lmhead_loss.hip: no [N, V] logits /
+                    dlogits in HBM; tokens with mask == 0 compacted out of the MFMA passes)
+      gemm          the reference's structure on the hot path's kernels: hipBLASLt bf16 logits ->
+                    fused loss rows -> hipBLASLt dh and dW GEMMs, over every token of the padded
+                    batch (the reference computes masked logits: accelerate_ppo_model.py:96-111)
+      gemm_compact  (masked shapes) the same kernels over the live tokens only: the live hidden
+                    rows (and their per-token inputs) gathered, the gemm route on a [1, live]
+                    batch, dh scattered back — the kernel-for-kernel comparison with `fused`
+                    (the live-row index is built once per batch outside the timed region:
+                    torch.nonzero syncs the host; the gathers and the scatter are timed)
+      dropin        the drop-in surface a reference user calls: PPOConfig.loss_from_hidden
+                    (autograd through lm_head_logprobs — saved-P plan — and the PPO loss) +
+                    loss.backward(), grads set to None each update (zero_grad(set_to_none)); no
+                    compaction (the reference's mask enters the loss only)"""
     B, T, V, H, masked = FROM_HIDDEN_SHAPES[name]
     g = torch.Generator(device=dev).manual_seed(4242)
     f = dict(generator=g, device=dev)
@@ -433,31 +445,67 @@ def from_hidden_leg(torch, P, dev, name, steps, rounds=3):
     if masked:
         lengths = torch.randint(1, T + 1, (B,), **f)
         mask = (torch.arange(T, device=dev)[None, :] < lengths[:, None]).long()
-    hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, dev, kl_coef=0.05, defer_tail=True)
+    cfg = P.PPOConfig()
+    hp = P.PPOHotPath(cfg, B, T, V, torch.bfloat16, dev, kl_coef=0.05, defer_tail=True)
     hp.experience_from_hidden(h, w, ref_h, w, labels, old_values, scores, lengths=lengths, mask=mask, route="fused")
+    hp.wait_stats()
+    routes = {"fused": lambda: hp.policy_loss_from_hidden(new_h, w, labels, values, old_values, mask=mask,
+                                                          route="fused"),
+              "gemm": lambda: hp.policy_loss_from_hidden(new_h, w, labels, values, old_values, mask=mask,
+                                                         route="gemm")}
+    nv = int(mask.sum().item()) if masked else B * T
+    hpc = None
+    if masked:  # gemm over the live tokens: a [1, nv] hot path fed the gathered rows
+        idx = mask.reshape(-1).nonzero().squeeze(1)
+        hpc = P.PPOHotPath(cfg, 1, nv, V, torch.bfloat16, dev, kl_coef=0.05, defer_tail=True)
+        hpc.adv_stats.copy_(hp.adv_stats)  # the batch's whitening record (Σmask = nv at [3])
+        dh_full = torch.zeros(B * T, H, dtype=torch.bfloat16, device=dev)
 
-    def upd(route):
-        hp.policy_loss_from_hidden(new_h, w, labels, values, old_values, mask=mask, route=route)
+        def gemm_compact():
+            hc = new_h.reshape(B * T, H).index_select(0, idx).view(1, nv, H)
+            for dst, src in ((hpc.lp_old, hp.lp_old), (hpc.adv_raw, hp.adv_raw), (hpc.returns, hp.returns)):
+                torch.index_select(src.reshape(-1), 0, idx, out=dst.view(-1))
+            take = lambda t: t.reshape(-1).index_select(0, idx).view(1, nv)  # noqa: E731
+            _, _, dhc, _, _ = hpc.policy_loss_from_hidden(hc, w, take(labels), take(values), take(old_values),
+                                                          route="gemm")
+            dh_full.index_copy_(0, idx, dhc.view(nv, H))  # masked rows stay zero
+        routes["gemm_compact"] = gemm_compact
+    # the drop-in: whitened advantages as get_advantages_and_returns hands them to the loss
+    mu, var = P.modeling.moments_to_mean_var(hp.adv_stats, unbiased=True)
+    adv_w = ((hp.adv_raw.double() - mu) * torch.rsqrt(var + 1e-8)).float()
+    hg = new_h.detach().clone().requires_grad_(True)
+    wg = w.detach().clone().requires_grad_(True)
+    vg = values.detach().clone().requires_grad_(True)
+    lp_old, rets = hp.lp_old.clone(), hp.returns.clone()
 
-    for route in ("fused", "gemm", "fused"):  # ~50 ms of load first: an idle chip runs slow (settle_and_warm)
-        for _ in range(8):
-            upd(route)
+    def dropin():
+        hg.grad = wg.grad = vg.grad = None
+        loss, _ = cfg.loss_from_hidden(hg, wg, vg, labels, lp_old, old_values, adv_w, rets, mask,
+                                       return_device_stats=True)
+        loss.backward()
+    routes["dropin"] = dropin
+
+    names = list(routes)
+    for route in names + names:  # ~50 ms of load first: an idle chip runs slow (settle_and_warm)
+        for _ in range(4):
+            routes[route]()
     hp.wait_stats()
     torch.cuda.synchronize()
-    times = {"fused": [], "gemm": []}
+    times = {n: [] for n in names}
     for r in range(rounds):
-        for route in (("fused", "gemm") if r % 2 == 0 else ("gemm", "fused")):
+        for route in names[r % len(names):] + names[:r % len(names)]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(steps):
-                upd(route)
+                routes[route]()
             hp.wait_stats()
+            if hpc is not None:
+                hpc.wait_stats()
             e1.record()
             torch.cuda.synchronize()
             times[route].append(e0.elapsed_time(e1) / steps)
-    nv = int(mask.sum().item()) if masked else B * T
-    fused_ms = sorted(times["fused"])[len(times["fused"]) // 2]
-    gemm_ms = sorted(times["gemm"])[len(times["gemm"]) // 2]
+    med = {n: sorted(v)[len(v) // 2] for n, v in times.items()}
+    fused_ms = med["fused"]
     # the plan the library ran for this workspace: saved P = 3 MFMA passes (S and O forward,
     # dSᵀ·h from the stored P), recompute = 4 (S again in the dW kernel)
     savep = P._lib.query("trlx_ppo_loss_from_hidden_plan", B * T, H, V, hp.lm_loss_ws.numel()) == 1
@@ -466,8 +514,13 @@ def from_hidden_leg(torch, P, dev, name, steps, rounds=3):
     ach = flop / (fused_ms * 1e-3) / 1e12
     out = {"shape": {"rows": B, "seq_len": T, "vocab": V, "hidden": H, "tokens": B * T, "live_tokens": nv,
                      "masked": masked},
-           "fused_ms_per_update": round(fused_ms, 4), "gemm_ms_per_update": round(gemm_ms, 4),
-           "fused_vs_gemm": round(gemm_ms / fused_ms, 4),
+           **{f"{n}_ms_per_update": round(v, 4) for n, v in med.items()},
+           "fused_vs_gemm": round(med["gemm"] / fused_ms, 4),
+           **({"fused_vs_gemm_compact": round(med["gemm_compact"] / fused_ms, 4)} if "gemm_compact" in med else {}),
+           "dropin_vs_fused": round(med["dropin"] / fused_ms, 4),
+           "ratios_note": ("fused_vs_gemm_compact is the kernel comparison (both routes over the live tokens); "
+                           "fused_vs_gemm also counts the masked tokens the reference's structure multiplies"
+                           if masked else "every token live: fused_vs_gemm is the kernel comparison"),
            "rounds_ms": {k: [round(v, 4) for v in vs] for k, vs in times.items()},
            "roofline": {"bound": "mfma", "achieved": round(ach, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "flop_per_update": flop,
@@ -477,7 +530,7 @@ def from_hidden_leg(torch, P, dev, name, steps, rounds=3):
                                 "count); recompute: + S again in the dW kernel (combine, compaction and loss "
                                 "tail included in the time)"},
            "steps_per_round": steps, "rounds": rounds}
-    del hp, h, w, ref_h, new_h
+    del hp, hpc, h, w, ref_h, new_h, hg, wg, vg
     torch.cuda.empty_cache()
     return out
 

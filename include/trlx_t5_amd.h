@@ -80,7 +80,11 @@ const char* trlx_last_error(void);
  *   "lmloss_splits"     fused loss forward vocab splits: 0 auto (the fullest last round), 1..8 fixed
  *   "lmloss_dw_tsplit"  fused loss dW: 0 auto (the last round's vocab blocks split over the tokens),
  *                       1 = no split, 2..16 = that many token splits
- *   "lmloss_fwd"        fused loss forward form: 0 auto (= 1), 1 = 32x32x16 wave pairs, 2 = 16x16x32 waves
+ *   "lmloss_fwd"        fused loss forward form: 0 / 2 = the 16x16x32 form (the only one built; the
+ *                       removed forms 1, 3, 4 are rejected with TRLX_ERR_ARG)
+ *   "lmloss_dw"         fused loss dW plan: 0 auto (saved P where the caller's buffers hold it),
+ *                       1 = recompute S (k_lmloss_dw), 4 = saved P (k_lmloss_dwp); 2, 3 rejected
+ *   "lmloss_dwp_rw"     saved-P dW rows per wave: 0 auto (= 2: 32 rows x H/2), 1 = 16 rows x H
  *   "store_policy"      gradient-row store cache policy: 0 auto (default: nt; sc1 for all-VGPR rows
  *                       launches writing > 1.5 GB), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
  * Results are identical up to fp32 summation order; only speed changes. */
@@ -368,7 +372,7 @@ int64_t trlx_ppo_loss_from_hidden_workspace_bytes(int64_t N, int64_t H, int64_t 
 /* The plan the PPO entries run for this shape and workspace size: 1 = saved P (three MFMA
  * passes: S and O forward, dSᵀ·h from the stored P), 0 = recompute (four: S recomputed in dW). */
 int trlx_ppo_loss_from_hidden_plan(int64_t N, int64_t H, int64_t V, int64_t lm_workspace_bytes);
-/* The smaller workspace trlx_lmhead_logprobs_bwd needs (no forward partials). */
+/* The smaller workspace trlx_lmhead_logprobs_bwd / _bwd_savep need (no forward partials). */
 int64_t trlx_lmhead_loss_bwd_workspace_bytes(int64_t N, int64_t H, int64_t V);
 /* The PPO loss from the policy's last hidden states: trlx_ppo_loss_rows's arguments with the
  * logits replaced by (hidden, weight) and dlogits by (dhidden, dweight) — same token records
@@ -417,6 +421,29 @@ int trlx_lmhead_logprobs_bwd(const void* hidden, int64_t ldh, const void* weight
                              int grad_dtype, const float* lse, const float* e, void* dhidden, int64_t lddh,
                              int dh_dtype, void* dweight, int dw_dtype, int64_t lddw, void* lm_workspace,
                              void* stream);
+/* The same pair, extended (replaces the same reference lines as the pair above:
+ * accelerate_ppo_model.py:96-118 through ppo_models.py:640 and modeling.py:37-41):
+ *   saved: NULL = the recompute plan (as above), or a region of trlx_lmhead_savep_bytes(N, H, V)
+ *          bytes (⌈V/64⌉·2⌈N/64⌉·4 KB + 128·N B: 0.62 GB at N = 6144, V = 50257 — the size of
+ *          bf16 logits) the forward fills with its bf16 P tiles and per-(split, token) records
+ *          and the caller keeps, unmodified, until the backward: the dW pass then reads P back
+ *          (3 MFMA passes in all) instead of recomputing S (4);
+ *   mask:  NULL = every token, or [N] int64: tokens with mask == 0 are compacted out of every
+ *          MFMA pass — their lp and lse are 0 and they get a zero dh and no share of dW (what the
+ *          PPO loss's own mask gives them: ppo_models.py:150-199 multiplies every lp term by it).
+ *          The backward takes the same mask (it rebuilds the same stable order).
+ * The "lmloss_splits" tuning must not change between the two calls (the records follow the
+ * forward's split plan).  lm_workspace as the pair above. */
+int64_t trlx_lmhead_savep_bytes(int64_t N, int64_t H, int64_t V);
+int trlx_lmhead_logprobs_fwd_ex(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
+                                int64_t H, int64_t V, const int64_t* labels, int64_t lb, const int64_t* mask,
+                                void* lp_out, int lp_dtype, float* lse_out, float* e_out, void* lm_workspace,
+                                void* saved, void* stream);
+int trlx_lmhead_logprobs_bwd_ex(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
+                                int64_t H, int64_t V, const int64_t* labels, int64_t lb, const int64_t* mask,
+                                const void* grad, int grad_dtype, const float* lse, const float* e, void* dhidden,
+                                int64_t lddh, int dh_dtype, void* dweight, int dw_dtype, int64_t lddw,
+                                void* lm_workspace, const void* saved, void* stream);
 
 /* ---------------------------------------------------------------- §8f rank 3: ILQL sampling step
  * One decode step of CausalLMWithValueHeads.generate (ilql_models.py:296-316) per row b:

@@ -308,33 +308,117 @@ def test_lm_head_logprobs_autograd_any_hidden_size():
     assert _rel(hg.grad, dh64) < 2e-2 and _rel(wg.grad, dw64) < 2e-2
 
 
-@pytest.mark.parametrize("form", [1, 2])
+@pytest.mark.parametrize("plan", ["saved_p", "recompute"])
 @pytest.mark.parametrize("N,H,V", [(200, 768, 7000), (70, 512, 33), (300, 768, 50257)])
-def test_lm_head_logprobs_forward_forms(form, N, H, V):
-    """Both forward forms (tuning lmloss_fwd: 1 = the 32x32x16 pair form with the group-sum
-    exchange, the default, 2 = the 16x16x32 one-wave-per-16-tokens form) against fp64, and
-    the restart path of each (a logit jump of ~80 from the 3rd tile on)."""
-    P._lib.set_tuning("lmloss_fwd", form)
-    try:
-        for jump in (False, True):
-            h, w, y = _operands(N, H, V, N + form)
-            if jump and V > 96:
-                wf = w.float()
-                dvec = h.float().mean(0)
-                wf[2 * 32:] += 80.0 * dvec / (dvec @ dvec)
-                w = wf.to(torch.bfloat16)
-            gout = torch.randn(N, generator=torch.Generator().manual_seed(form))
-            hg = h.to(DEV).requires_grad_(True)
-            wg = w.to(DEV).requires_grad_(True)
-            lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32)
-            (lp * gout.to(DEV)).sum().backward()
-            torch.cuda.synchronize()
-            lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
-            torch.testing.assert_close(lp.detach().double(), lp64, rtol=1e-5, atol=1e-4)
-            assert _rel(hg.grad, dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
-    finally:
-        P._lib.set_tuning("lmloss_fwd", 0)
+def test_lm_head_logprobs_restart_shapes(plan, N, H, V):
+    """The forward (16x16x32 form) against fp64 on both dW plans, with and without the restart
+    path (a logit jump of ~80 from the 3rd tile on: the restarted blocks rewrite their P tiles
+    and offsets, which the saved-P backward then reads)."""
+    for jump in (False, True):
+        h, w, y = _operands(N, H, V, N + V)
+        if jump and V > 96:
+            wf = w.float()
+            dvec = h.float().mean(0)
+            wf[2 * 32:] += 80.0 * dvec / (dvec @ dvec)
+            w = wf.to(torch.bfloat16)
+        gout = torch.randn(N, generator=torch.Generator().manual_seed(2))
+        hg = h.to(DEV).requires_grad_(True)
+        wg = w.to(DEV).requires_grad_(True)
+        lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32, plan=plan)
+        (lp * gout.to(DEV)).sum().backward()
+        torch.cuda.synchronize()
+        lp64, dh64, dw64 = _fp64_grads(h, w, y, gout)
+        torch.testing.assert_close(lp.detach().double(), lp64, rtol=1e-5, atol=1e-4)
+        assert _rel(hg.grad, dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
 
+
+def test_lm_head_logprobs_plans_agree_and_frozen_operands():
+    """The two dW plans on the same call: lp and dh bit-identical (the plans differ in the dW
+    pass only), dW to the bf16 rounding of P / dS.  A frozen lm_head (weight without grad: no dW
+    pass, no P kept) and detached hidden states (dh not requested: the combine writes no dh)
+    each return the other gradient as in the full call, and None for theirs."""
+    N, H, V = 333, 768, 5000
+    h, w, y = _operands(N, H, V, 19)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(9)).to(DEV)
+    outs = {}
+    for plan in ("saved_p", "recompute"):
+        hg = h.to(DEV).requires_grad_(True)
+        wg = w.to(DEV).requires_grad_(True)
+        lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32, plan=plan)
+        (lp * gout).sum().backward()
+        torch.cuda.synchronize()
+        outs[plan] = (lp.detach(), hg.grad, wg.grad)
+    a, b = outs["saved_p"], outs["recompute"]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert _rel(a[2], b[2]) < 4e-3
+    # frozen lm_head: dh only
+    hg = h.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(hg, w.to(DEV), y.to(DEV), out_dtype=torch.float32)
+    (lp * gout).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(hg.grad, a[1])
+    # hidden detached: dW only (saved P), equal to the full call's
+    wg = w.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(h.to(DEV), wg, y.to(DEV), out_dtype=torch.float32)
+    (lp * gout).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(wg.grad, a[2])
+    # and against torch autograd of the reference structure in fp32 (the same operands)
+    _, dh64, dw64 = _fp64_grads(h, w, y, gout.cpu())
+    assert _rel(a[1], dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
+
+
+@pytest.mark.parametrize("plan", ["saved_p", "recompute"])
+@pytest.mark.parametrize("N,H,V", [(300, 768, 5000), (6144, 768, 32128), (77, 512, 1031)])
+def test_lm_head_logprobs_mask_compacts(plan, N, H, V):
+    """lm_head_logprobs(mask=...): the masked tokens are compacted out of the MFMA passes
+    (their hidden rows NaN-poisoned here: never read) — lp = 0 and zero dh there, the live
+    tokens' lp / dh and the dW over the live tokens against fp64 of the live rows alone, on both
+    plans; the no-grad path returns the same lp."""
+    h, w, y = _operands(N, H, V, N + 5)
+    g = torch.Generator().manual_seed(N)
+    m = (torch.rand(N, generator=g) < 0.55).long()
+    m[0] = 1
+    gout = torch.randn(N, generator=g)
+    live = m.bool()
+    hd = h.to(DEV).masked_fill((m == 0).to(DEV)[:, None], float("nan")).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(hd, wg, y.to(DEV), out_dtype=torch.float32, plan=plan, mask=m.to(DEV))
+    (lp * gout.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert (lp.detach().cpu()[~live] == 0).all() and (hd.grad.cpu()[~live] == 0).all()
+    assert torch.isfinite(hd.grad).all() and torch.isfinite(wg.grad).all()
+    lp64, dh64, dw64 = _fp64_grads(h[live], w, y[live], gout[live])
+    torch.testing.assert_close(lp.detach()[live.to(DEV)].double(), lp64, rtol=1e-5, atol=2e-5)
+    assert _rel(hd.grad[live.to(DEV)], dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
+    with torch.no_grad():
+        lp_ng = P.lm_head_logprobs(h.to(DEV), w.to(DEV), y.to(DEV), out_dtype=torch.float32, mask=m.to(DEV))
+    torch.testing.assert_close(lp_ng, lp.detach(), rtol=1e-5, atol=2e-5)
+
+
+def test_lm_head_logprobs_auto_plan_falls_back_when_p_does_not_fit(monkeypatch):
+    """plan="auto": when the saved-P region cannot be allocated (its size made impossible
+    here) the call takes the recompute plan and gives the recompute plan's bits."""
+    N, H, V = 200, 512, 3000
+    h, w, y = _operands(N, H, V, 29)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(1)).to(DEV)
+
+    def run(plan):
+        hg = h.to(DEV).requires_grad_(True)
+        wg = w.to(DEV).requires_grad_(True)
+        lp = P.lm_head_logprobs(hg, wg, y.to(DEV), out_dtype=torch.float32, plan=plan)
+        (lp * gout).sum().backward()
+        torch.cuda.synchronize()
+        return hg.grad, wg.grad
+
+    want = run("recompute")
+    real_query = P._lib.query
+    monkeypatch.setattr(P._lib, "query", lambda name, *a: (1 << 52) if name == "trlx_lmhead_savep_bytes"
+                        else real_query(name, *a))
+    got = run("auto")
+    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+    with pytest.raises(torch.cuda.OutOfMemoryError):
+        run("saved_p")
 
 
 # ------------------------------------------------------------------ the softmax halves, checked by themselves
@@ -345,9 +429,10 @@ def test_lm_head_logprobs_forward_forms(form, N, H, V):
 import lmloss_checks as C  # noqa: E402
 
 
-def _fwd_saved_bwd(h, w, y, gout, dh_dtype, dw_dtype):
-    """trlx_lmhead_logprobs_fwd_saved + trlx_lmhead_logprobs_bwd through the C ABI on this
-    thread (lp, lse, the saved E, dh, dW)."""
+def _fwd_saved_bwd(h, w, y, gout, dh_dtype, dw_dtype, plan="recompute"):
+    """The drop-in pair through the C ABI on this thread (lp, lse, the saved E, dh, dW):
+    trlx_lmhead_logprobs_fwd_saved + _bwd (recompute plan) or _fwd_savep + _bwd_savep
+    (saved_p: the forward's P tiles kept in a region of trlx_lmhead_savep_bytes)."""
     N, H = h.shape
     V = w.shape[0]
     L = P._lib
@@ -356,14 +441,24 @@ def _fwd_saved_bwd(h, w, y, gout, dh_dtype, dw_dtype):
     lp, lse, e = torch.empty(N, **f32), torch.empty(N, **f32), torch.empty((N, H), **f32)
     ws = torch.empty(L.query("trlx_lmhead_loss_workspace_bytes", N, H, V), dtype=torch.uint8, device=DEV)
     s = torch.cuda.current_stream(DEV).cuda_stream
-    L.call("trlx_lmhead_logprobs_fwd_saved", hd.data_ptr(), H, wd.data_ptr(), H, N, H, V, yd.data_ptr(), 1,
-           lp.data_ptr(), L.F32, lse.data_ptr(), e.data_ptr(), ws.data_ptr(), s)
+    fwd = (hd.data_ptr(), H, wd.data_ptr(), H, N, H, V, yd.data_ptr(), 1, lp.data_ptr(), L.F32, lse.data_ptr(),
+           e.data_ptr(), ws.data_ptr())
+    saved = None
+    if plan == "saved_p":
+        saved = torch.empty(L.query("trlx_lmhead_savep_bytes", N, H, V), dtype=torch.uint8, device=DEV)
+        L.call("trlx_lmhead_logprobs_fwd_ex", *fwd[:9], None, *fwd[9:], saved.data_ptr(), s)
+    else:
+        L.call("trlx_lmhead_logprobs_fwd_saved", *fwd, s)
+    del ws  # the forward's partials are not needed by the backward
     dh = torch.empty((N, H), dtype=dh_dtype, device=DEV)
     dw = torch.empty((V, H), dtype=dw_dtype, device=DEV)
     wsb = torch.empty(L.query("trlx_lmhead_loss_bwd_workspace_bytes", N, H, V), dtype=torch.uint8, device=DEV)
-    L.call("trlx_lmhead_logprobs_bwd", hd.data_ptr(), H, wd.data_ptr(), H, N, H, V, yd.data_ptr(), 1, gd.data_ptr(),
-           L.F32, lse.data_ptr(), e.data_ptr(), dh.data_ptr(), H, L.dtype_code(dh), dw.data_ptr(), L.dtype_code(dw), H,
-           wsb.data_ptr(), s)
+    bwd = (hd.data_ptr(), H, wd.data_ptr(), H, N, H, V, yd.data_ptr(), 1, gd.data_ptr(), L.F32, lse.data_ptr(),
+           e.data_ptr(), dh.data_ptr(), H, L.dtype_code(dh), dw.data_ptr(), L.dtype_code(dw), H, wsb.data_ptr())
+    if saved is not None:
+        L.call("trlx_lmhead_logprobs_bwd_ex", *bwd[:9], None, *bwd[9:], saved.data_ptr(), s)
+    else:
+        L.call("trlx_lmhead_logprobs_bwd", *bwd, s)
     torch.cuda.synchronize()
     return lp, lse, e, dh, dw
 
@@ -374,32 +469,30 @@ def _halves_operands(kind, N, H, V, seed):
     return _operands(N, H, V, seed)
 
 
-@pytest.mark.parametrize("kind,N,H,V,form", [
-    ("flat", 6144, 768, 50257, 0), ("peaked", 6144, 768, 50257, 0), ("peaked", 6144, 768, 50257, 2),
-    ("flat", 12288, 768, 32128, 0), ("peaked", 12288, 768, 32128, 0), ("peaked", 1000, 512, 5000, 0),
-    ("flat", 333, 768, 1031, 2)])
-def test_lm_head_loss_side_halves(kind, N, H, V, form):
-    """The forward's saved E, dh and dW against fp64 (C2: V 50257, C3: V 32128 at their token
-    counts; flat and peaked softmax; both forward forms), each half by itself
-    (tests/lmloss_checks.py): fp32 outputs (dh sees E at 2^-7 of |g|·‖E‖) and bf16 outputs."""
-    h, w, y = _halves_operands(kind, N, H, V, N + V + form)
+@pytest.mark.parametrize("plan", ["saved_p", "recompute"])
+@pytest.mark.parametrize("kind,N,H,V", [
+    ("flat", 6144, 768, 50257), ("peaked", 6144, 768, 50257), ("flat", 12288, 768, 32128),
+    ("peaked", 12288, 768, 32128), ("peaked", 1000, 512, 5000), ("flat", 333, 768, 1031), ("flat", 17, 768, 100),
+    ("flat", 70, 512, 33)])
+def test_lm_head_loss_side_halves(kind, N, H, V, plan):
+    """The drop-in pair's saved E, dh and dW against fp64 (C2: V 50257, C3: V 32128 at their
+    token counts; flat and peaked softmax; ragged token counts and vocab sizes off the tiles;
+    both dW plans), each half by itself (tests/lmloss_checks.py): fp32 outputs (dh sees E at
+    2^-7 of |g|·‖E‖) and bf16 outputs."""
+    h, w, y = _halves_operands(kind, N, H, V, N + V)
     gout = torch.randn(N, generator=torch.Generator().manual_seed(7))
     t = C.fp64_truth(h.to(DEV), w.to(DEV), y.to(DEV), gout.to(DEV))
     if kind == "peaked":  # the case is what it says: the label's probability is far from 1/V
         p_lab = torch.exp(t["lp"])
         assert float(p_lab.median()) > 0.05, float(p_lab.median())
-    P._lib.set_tuning("lmloss_fwd", form)
-    try:
-        for dh_dt, dw_dt in ((torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)):
-            lp, lse, e, dh, dw = _fwd_saved_bwd(h, w, y, gout, dh_dt, dw_dt)
-            torch.testing.assert_close(lp.double(), t["lp"], rtol=1e-5, atol=2e-5)
-            torch.testing.assert_close(lse.double(), t["lse"], rtol=1e-6, atol=2e-5)
-            errs = C.e_errors(e, t["e"])
-            errs.update(C.dw_errors(dw, t["dw"], y))
-            errs.update(C.dh_errors(dh, t["dh"], gout, t["e"], fp32_out=dh_dt == torch.float32))
-            C.assert_within(errs, f"{kind} N={N} V={V} form={form} out={dh_dt}")
-    finally:
-        P._lib.set_tuning("lmloss_fwd", 0)
+    for dh_dt, dw_dt in ((torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)):
+        lp, lse, e, dh, dw = _fwd_saved_bwd(h, w, y, gout, dh_dt, dw_dt, plan)
+        torch.testing.assert_close(lp.double(), t["lp"], rtol=1e-5, atol=2e-5)
+        torch.testing.assert_close(lse.double(), t["lse"], rtol=1e-6, atol=2e-5)
+        errs = C.e_errors(e, t["e"])
+        errs.update(C.dw_errors(dw, t["dw"], y))
+        errs.update(C.dh_errors(dh, t["dh"], gout, t["e"], fp32_out=dh_dt == torch.float32))
+        C.assert_within(errs, f"{kind} N={N} V={V} plan={plan} out={dh_dt}")
 
 
 def _hot_path_halves(x, B, T, V, H, masked, label):
@@ -500,103 +593,6 @@ def test_hot_path_saved_p_plans(splits, tsplit):
         torch.testing.assert_close(b[5], a[5], rtol=1e-5, atol=1e-5)
         assert torch.equal(b[2], a[2])  # dh comes from the combine: the plans differ in dW only
         assert _rel(b[3], a[3]) < 4e-3
-
-
-@pytest.mark.parametrize("kind,N,H,V", [("flat", 6144, 768, 50257), ("peaked", 6144, 768, 50257),
-                                        ("peaked", 2000, 768, 32128), ("flat", 333, 768, 1031),
-                                        ("peaked", 1000, 512, 5000), ("flat", 70, 512, 33), ("flat", 17, 768, 100)])
-@pytest.mark.parametrize("fwd,dw", [(3, 2), (1, 2), (3, 1), (4, 3)])
-def test_lm_head_loss_h_sliced_forms(kind, N, H, V, fwd, dw):
-    """The H-sliced forms (tunings lmloss_fwd = 3, lmloss_dw = 2: each wave owns a quarter of
-    the hidden dimension for its 64 register rows, 16-row tiles, one barrier per tile) against
-    fp64 with the halves checks — ragged token counts (17, 70, 333: partial 16-token tiles and
-    64-token blocks), vocab sizes off the 16-row tile (33, 100, 1031, 50257) and both hidden
-    sizes."""
-    h, w, y = _halves_operands(kind, N, H, V, 7 * N + V)
-    gout = torch.randn(N, generator=torch.Generator().manual_seed(17))
-    t = C.fp64_truth(h.to(DEV), w.to(DEV), y.to(DEV), gout.to(DEV))
-    P._lib.set_tuning("lmloss_fwd", fwd)
-    P._lib.set_tuning("lmloss_dw", dw)
-    try:
-        for dh_dt, dw_dt in ((torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16)):
-            lp, lse, e, dh, dwt = _fwd_saved_bwd(h, w, y, gout, dh_dt, dw_dt)
-            torch.testing.assert_close(lp.double(), t["lp"], rtol=1e-5, atol=2e-5)
-            torch.testing.assert_close(lse.double(), t["lse"], rtol=1e-6, atol=2e-5)
-            errs = C.e_errors(e, t["e"])
-            errs.update(C.dw_errors(dwt, t["dw"], y))
-            errs.update(C.dh_errors(dh, t["dh"], gout, t["e"], fp32_out=dh_dt == torch.float32))
-            C.assert_within(errs, f"H-sliced fwd={fwd} dw={dw} {kind} N={N} H={H} V={V} out={dh_dt}")
-    finally:
-        P._lib.set_tuning("lmloss_fwd", 0)
-        P._lib.set_tuning("lmloss_dw", 0)
-
-
-@pytest.mark.parametrize("fwd,dw", [(3, 2), (4, 3)])
-@pytest.mark.parametrize("splits,tsplit", [(1, 1), (3, 2), (8, 5), (5, 16)])
-def test_lm_head_loss_h_sliced_plans(splits, tsplit, fwd, dw):
-    """Forced grid plans on the H-sliced forms: vocab splits of the forward, token splits of
-    the dW kernel's last round (fp32 partials + the fixed-order reduce), and the restart of
-    the fixed-offset softmax (a logit jump of ~80 from the 3rd tile on)."""
-    N, H, V = 200, 768, 7000
-    for jump in (False, True):
-        h, w, y = _operands(N, H, V, 5 + jump)
-        if jump:
-            wf = w.float()
-            dvec = h.float().mean(0)
-            wf[2 * 16:] += 80.0 * dvec / (dvec @ dvec)
-            w = wf.to(torch.bfloat16)
-        gout = torch.randn(N, generator=torch.Generator().manual_seed(6))
-        t = C.fp64_truth(h.to(DEV), w.to(DEV), y.to(DEV), gout.to(DEV))
-        P._lib.set_tuning("lmloss_fwd", fwd)
-        P._lib.set_tuning("lmloss_dw", dw)
-        P._lib.set_tuning("lmloss_splits", splits)
-        P._lib.set_tuning("lmloss_dw_tsplit", tsplit)
-        try:
-            lp, lse, e, dh, dwt = _fwd_saved_bwd(h, w, y, gout, torch.float32, torch.float32)
-        finally:
-            for k in ("lmloss_fwd", "lmloss_dw", "lmloss_splits", "lmloss_dw_tsplit"):
-                P._lib.set_tuning(k, 0)
-        assert torch.isfinite(lp).all() and torch.isfinite(dh).all()
-        torch.testing.assert_close(lp.double(), t["lp"], rtol=1e-5, atol=1e-4)
-        errs = C.e_errors(e, t["e"])
-        errs.update(C.dw_errors(dwt, t["dw"], y))
-        errs.update(C.dh_errors(dh, t["dh"], gout, t["e"], fp32_out=True))
-        C.assert_within(errs, f"H-sliced plans splits={splits} tsplit={tsplit} jump={jump}")
-
-
-@pytest.mark.parametrize("B,T,V,H,masked", [(128, 48, 50257, 768, False), (256, 48, 32128, 768, True),
-                                            (8, 20, 5000, 512, True)])
-def test_hot_path_h_sliced_matches_row_split(B, T, V, H, masked):
-    """The PPO route (compaction of masked tokens, the PPO combine) on the H-sliced forms
-    against the row-split forms on the same step: loss, stats and dvalues equal to fp32
-    summation order, dh / dW to the bf16 rounding of P / dS."""
-    x = _ppo_inputs(B, T, V, H, 900 + B, masked)
-    d = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in x.items()}
-    if masked:
-        d["new_h"] = d["new_h"].masked_fill((d["mask"] == 0)[..., None], float("nan"))
-    outs = {}
-    for fwd, dw in ((1, 1), (3, 2), (4, 3), (0, 0)):
-        P._lib.set_tuning("lmloss_fwd", fwd)
-        P._lib.set_tuning("lmloss_dw", dw)
-        try:
-            hp = P.PPOHotPath(P.PPOConfig(), B, T, V, torch.bfloat16, DEV, kl_coef=0.05)
-            o = hp.step_from_hidden(d["h"], d["w"], d["ref_h"], d["w"], d["new_h"], d["labels"], d["old_values"],
-                                    d["values"], d["scores"], lengths=d["lengths"], mask=d["mask"], route="fused",
-                                    loss_route="fused", grad_dtype=torch.float32)
-            torch.cuda.synchronize()
-            outs[fwd] = [t.clone() for t in o] + [hp.lp_new.clone()]
-        finally:
-            P._lib.set_tuning("lmloss_fwd", 0)
-            P._lib.set_tuning("lmloss_dw", 0)
-    a = outs[1]
-    for f in (3, 4, 0):  # 0: the defaults (16x16 forward, saved-P dW)
-        b = outs[f]
-        torch.testing.assert_close(b[0], a[0], rtol=1e-5, atol=1e-6)
-        torch.testing.assert_close(b[1], a[1], rtol=1e-4, atol=1e-6)
-        torch.testing.assert_close(b[4], a[4], rtol=1e-5, atol=1e-7)
-        torch.testing.assert_close(b[5], a[5], rtol=1e-5, atol=1e-5)
-        assert _rel(b[2], a[2]) < 4e-3 and _rel(b[3], a[3]) < 4e-3
-        assert torch.isfinite(b[2]).all() and torch.isfinite(b[3]).all()
 
 
 def test_lm_head_logprobs_autograd_no_device_allocation_in_steady_state():

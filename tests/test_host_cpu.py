@@ -210,6 +210,43 @@ def test_ilql_refuses_cpu_tensors():
         cfg.loss((torch.randn(B, L, V), (qs, qs, torch.randn(B, L, 1))), b)
 
 
+def test_tuning_rejects_removed_forms_and_restores():
+    """The dropped loss-side forms (round-5 H-sliced engines, the 32x32 pair forward) are no
+    longer selectable; _lib.tuning restores the previous knob values (host-only calls)."""
+    import trlx_t5_amd as P
+    L = P._lib
+    for key, val in (("lmloss_fwd", 1), ("lmloss_fwd", 3), ("lmloss_fwd", 4), ("lmloss_dw", 2), ("lmloss_dw", 3)):
+        with pytest.raises(ValueError):
+            L.set_tuning(key, val)
+    L.set_tuning("lmloss_fwd", 2)
+    L.set_tuning("lmloss_fwd", 0)
+    L.set_tuning("lmloss_dw", 4)
+    with L.tuning(lmloss_dw=1, lmloss_splits=3):
+        assert L._TUNED["lmloss_dw"] == 1 and L._TUNED["lmloss_splits"] == 3
+    assert L._TUNED["lmloss_dw"] == 4 and L._TUNED["lmloss_splits"] == 0
+    with pytest.raises(RuntimeError):
+        with L.tuning(lmloss_dw=1):
+            raise RuntimeError("inside")
+    assert L._TUNED["lmloss_dw"] == 4
+    L.set_tuning("lmloss_dw", 0)
+
+
+def test_savep_region_sizes():
+    """The saved-P region of the drop-in pair: the P tiles (⌈V/64⌉ x 2⌈N/64⌉ x 4 KB, the size of
+    bf16 logits rounded to tiles) + 8 records of 16 B per token; the PPO entries' saved-P
+    workspace holds the same on top of the recompute plan's."""
+    import trlx_t5_amd as P
+    q = P._lib.query
+    N, H, V = 6144, 768, 50257
+    pbytes = ((V + 63) // 64) * 2 * ((N + 63) // 64) * 4096
+    assert q("trlx_lmhead_savep_bytes", N, H, V) == pbytes + 8 * N * 16
+    assert pbytes >= 2 * N * V
+    big, small = q("trlx_ppo_loss_from_hidden_workspace_bytes", N, H, V), q("trlx_lmhead_loss_workspace_bytes", N, H, V)
+    assert big - small >= pbytes + 8 * N * 16
+    assert q("trlx_ppo_loss_from_hidden_plan", N, H, V, big) == 1
+    assert q("trlx_ppo_loss_from_hidden_plan", N, H, V, small) == 0
+
+
 def test_hot_path_refuses_bad_loss_norm():
     import trlx_t5_amd as P
     with pytest.raises(ValueError):

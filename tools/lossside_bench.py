@@ -82,11 +82,7 @@ def main():
         hp.policy_loss_from_hidden(new_h, w, labels, values, old_values, mask=mask)
 
     def fused_recompute():  # the dW kernel recomputing S^T (k_lmloss_dw) instead of the saved P
-        P._lib.set_tuning("lmloss_dw", 1)
-        try:
-            fused()
-        finally:
-            P._lib.set_tuning("lmloss_dw", 0)
+        hp.policy_loss_from_hidden(new_h, w, labels, values, old_values, mask=mask, plan="recompute")
 
     routes = {"gemm": gemm, "fused": fused, "fused_recompute": fused_recompute}
     names = args.routes.split(",")
@@ -105,14 +101,23 @@ def main():
                 b.record()
             torch.cuda.synchronize()
             res[n].append(statistics.median(a.elapsed_time(b) for a, b in evs) * 1e3)
-    flop = 2.0 * N * V * H
-    out = {"config": args.config, "N": N, "V": V, "H": H, "masked": masked,
+    # one N·V·H multiply-add pass: the fused route over the live (mask != 0) tokens it keeps,
+    # the gemm route over every token; the passes each route's plan runs (bench.py's count)
+    nv = int(mask.sum().item()) if mask is not None else N
+    flop_live, flop_all = 2.0 * nv * V * H, 2.0 * N * V * H
+    savep = P._lib.query("trlx_ppo_loss_from_hidden_plan", N, H, V, hp.lm_loss_ws.numel()) == 1
+    out = {"config": args.config, "N": N, "live_tokens": nv, "V": V, "H": H, "masked": masked,
            "us_per_call": {n: [round(x, 1) for x in v] for n, v in res.items()}}
+    if "gemm" in res:
+        out["gemm_tflops_3pass"] = round(3 * flop_all / (min(res["gemm"]) * 1e-6) / 1e12, 1)
+    if "fused" in res:
+        passes = 3 if savep else 4
+        out["fused_plan"] = "saved_p" if savep else "recompute"
+        out[f"fused_tflops_{passes}pass"] = round(passes * flop_live / (min(res["fused"]) * 1e-6) / 1e12, 1)
+    if "fused_recompute" in res:
+        out["fused_recompute_tflops_4pass"] = round(4 * flop_live / (min(res["fused_recompute"]) * 1e-6) / 1e12, 1)
     if "gemm" in res and "fused" in res:
-        gm, fm = min(res["gemm"]), min(res["fused"])
-        out["speedup_fused_vs_gemm"] = round(gm / fm, 3)
-        out["fused_tflops_4pass"] = round(4 * flop / (fm * 1e-6) / 1e12, 1)
-        out["gemm_tflops_3pass"] = round(3 * flop / (gm * 1e-6) / 1e12, 1)
+        out["speedup_fused_vs_gemm"] = round(min(res["gemm"]) / min(res["fused"]), 3)
     print(json.dumps(out), flush=True)
 
 

@@ -6,6 +6,7 @@ point raises.  torch is imported first so the HIP runtime the library links agai
 (libamdhip64.so.7) resolves to the one torch already loaded — the library then launches
 on torch's streams directly.
 """
+import contextlib
 import ctypes
 import os
 
@@ -142,6 +143,12 @@ SIGNATURES = {
     "trlx_lmhead_logprobs_bwd": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp,
                                           _c_int, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_i64, _c_vp,
                                           _c_vp]),
+    "trlx_lmhead_savep_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64]),
+    "trlx_lmhead_logprobs_fwd_ex": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
+                                             _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "trlx_lmhead_logprobs_bwd_ex": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64,
+                                             _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_int,
+                                             _c_i64, _c_vp, _c_vp, _c_vp]),
     "trlx_lmhead_set_variant": (_c_int, [_c_int]),
     "trlx_lmhead_logprobs": (_c_int, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp,
                                       _c_int, _c_vp, _c_vp, _c_vp]),
@@ -229,9 +236,29 @@ def call(name, *args):
     return rc
 
 
+_TUNED = {}  # the values set through this binding (the library keeps no getter); unset = 0 (auto)
+
+
 def set_tuning(key: str, value: int):
-    """Launch-geometry knob (see trlx_set_tuning in include/trlx_t5_amd.h)."""
+    """Launch-geometry knob (see trlx_set_tuning in include/trlx_t5_amd.h).  The knobs are
+    process-wide (common.h TuneKnob): a value set here reaches every host thread's launches,
+    autograd's backward thread included."""
     call("trlx_set_tuning", key.encode(), int(value))
+    _TUNED[key] = int(value)
+
+
+@contextlib.contextmanager
+def tuning(**knobs):
+    """Set knobs for the duration of a block and restore the values they had before (the ones
+    set through set_tuning, else 0 = auto), also when the block raises."""
+    prev = {k: _TUNED.get(k, 0) for k in knobs}
+    try:
+        for k, v in knobs.items():
+            set_tuning(k, v)
+        yield
+    finally:
+        for k, v in prev.items():
+            set_tuning(k, v)
 
 
 def query(name, *args):

@@ -313,19 +313,21 @@ class PPOConfig:
         return adv.detach(), ret
 
     # -------------------------------------------------------------- A6
-    def loss(self, logprobs, values, old_logprobs, old_values, advantages, returns, mask):
+    def loss(self, logprobs, values, old_logprobs, old_values, advantages, returns, mask,
+             return_device_stats=False):
         """PPO clipped-surrogate + clipped value loss (ppo_models.py:141-199).
 
-        Returns (loss, stats) with the reference's flattened stats keys and value types.
-        Gradients flow to `logprobs` and `values` (closed form, computed in the forward
+        Returns (loss, stats) with the reference's flattened stats keys and value types (or the
+        fp32 device stats vector in STATS_KEYS order when return_device_stats=True: no host
+        sync).  Gradients flow to `logprobs` and `values` (closed form, computed in the forward
         kernel, scaled by grad_output in backward)."""
         _lib.require_cuda(logprobs, values, old_logprobs, old_values, advantages, returns)
         loss, stats = _PPOLoss.apply(logprobs, values, old_logprobs, old_values, advantages, returns, mask,
                                      self.cliprange, self.cliprange_value, self.vf_coef)
-        return loss, stats_dict(stats)
+        return loss, (stats if return_device_stats else stats_dict(stats))
 
     def loss_from_hidden(self, hidden, weight, values, labels, old_logprobs, old_values, advantages, returns,
-                         mask=None):
+                         mask=None, plan="auto", return_device_stats=False):
         """The loss side from the policy's last hidden states:
             self.loss(logprobs_from_logits(hidden @ weight.T, labels), values, ...)
         (accelerate_ppo_model.py:96-118 with the lm_head of ppo_models.py:640 / :274), the
@@ -333,10 +335,15 @@ class PPOConfig:
         feeds the PPO loss kernels, and backward() delivers d hidden, d weight (lm_head) and
         d values.  hidden [.., H] / weight [V, H] bf16 (H in lm_head.GRAD_HIDDEN_SIZES: the fused
         backward; other H: hipBLASLt bf16 logits + the row kernels, the reference's structure).
+        plan: lm_head_logprobs' dW plan ("auto": the forward's bf16 P kept for the backward — 3
+        MFMA passes, 2·N·V bytes held until backward — falling back to recomputing S when that
+        buffer cannot be allocated; "saved_p"; "recompute").
         Returns (loss, stats) like loss(); logprobs are kept in fp32 (the reference's bf16
         logits give bf16 logprobs)."""
-        lp = lm_head_logprobs(hidden, weight, labels, out_dtype=torch.float32)
-        return self.loss(lp, values, old_logprobs, old_values, advantages, returns, mask)
+        # the loss multiplies every lp term by `mask`: the fused lm_head skips the masked tokens
+        lp = lm_head_logprobs(hidden, weight, labels, out_dtype=torch.float32, plan=plan, mask=mask)
+        return self.loss(lp, values, old_logprobs, old_values, advantages, returns, mask,
+                         return_device_stats=return_device_stats)
 
     def loss_from_logits(self, logits, values, labels, old_logprobs, old_values, advantages, returns,
                          mask=None, adv_stats=None, unbiased=True, return_device_stats=False):

@@ -154,6 +154,9 @@ class PPOHotPath:
         self.dlogits = None
         self.lm_ws = None  # lm_head partials workspace (experience_from_hidden)
         self.lm_logits = None  # [2, B, T, V] bf16 logits of the GEMM route (experience_from_hidden)
+        self.lm_loss_ws = None  # the fused loss side's workspace (policy_loss_from_hidden)
+        self.distributed = False  # whether the current whitening record is all-reduced (set per experience)
+        self._loss_ws_fallback = False  # plan "auto" fell back to the recompute plan (allocation failed)
         self.timers = None  # optional {name: [(start_event, end_event), ...]} (recorded when set)
         self.timer_names = None  # optional subset of launch names to instrument (None = all)
         self._conv = {}  # int64 buffers for labels / mask / lengths given in another integer dtype
@@ -681,8 +684,50 @@ class PPOHotPath:
     # -------------------------------------------------------------- K2 from hidden states (§8f-2, loss side)
     LOSS_FROM_HIDDEN_SIZES = (512, 768)
 
+    def _loss_from_hidden_route(self, hidden, weight, grad_dtype, route, plan="auto"):
+        """policy_loss_from_hidden's argument checks (shapes, dtypes, route, plan) -> the route it
+        will take; run before any launch (pipeline_step_from_hidden: when the batch is submitted)."""
+        B, T, V = self.B, self.T, self.V
+        if hidden.dim() != 3 or tuple(hidden.shape[:2]) != (B, T) or weight.dim() != 2 or weight.shape[0] != V or \
+                weight.shape[1] != hidden.shape[2] or hidden.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+            raise ValueError(f"hidden {tuple(hidden.shape)}/{hidden.dtype} and weight {tuple(weight.shape)}/"
+                             f"{weight.dtype} do not match the hot path ({B},{T},H) x ({V},H) bf16")
+        H = hidden.shape[2]
+        if grad_dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("grad_dtype must be bf16 or fp32")
+        if route not in ("auto", "fused", "gemm"):
+            raise ValueError(f"route must be auto, fused or gemm, not {route!r}")
+        if plan not in ("auto", "saved_p", "recompute"):
+            raise ValueError(f"plan must be auto, saved_p or recompute, not {plan!r}")
+        if route == "auto":
+            route = "fused" if H in self.LOSS_FROM_HIDDEN_SIZES else "gemm"
+        if route == "fused" and H not in self.LOSS_FROM_HIDDEN_SIZES:
+            raise ValueError(f"policy_loss_from_hidden: fused route not built for hidden size {H} "
+                             f"{self.LOSS_FROM_HIDDEN_SIZES} (route='gemm' takes any H)")
+        return route
+
+    def _loss_workspace(self, N, H, V, plan):
+        """The fused loss side's workspace and the byte count to pass (the C side picks the
+        saved-P plan when it holds the P tiles).  auto: saved P unless its 2·N·V-byte buffer
+        cannot be allocated — then the recompute plan, sticky until release_loss_workspace()."""
+        small = _lib.query("trlx_lmhead_loss_workspace_bytes", N, H, V)
+        big = _lib.query("trlx_ppo_loss_from_hidden_workspace_bytes", N, H, V)
+        want = small if (plan == "recompute" or (plan == "auto" and self._loss_ws_fallback)) else big
+        cur = getattr(self, "lm_loss_ws", None)
+        if cur is None or cur.numel() < want:
+            self.lm_loss_ws = None
+            try:
+                self.lm_loss_ws = torch.empty(want, dtype=torch.uint8, device=self.device)
+            except torch.cuda.OutOfMemoryError:
+                if plan != "auto" or want == small:
+                    raise
+                self._loss_ws_fallback = True
+                self.lm_loss_ws = cur if cur is not None and cur.numel() >= small else \
+                    torch.empty(small, dtype=torch.uint8, device=self.device)
+        return self.lm_loss_ws, (min(small, self.lm_loss_ws.numel()) if want == small else self.lm_loss_ws.numel())
+
     def policy_loss_from_hidden(self, hidden, weight, labels, values, old_values, mask=None,
-                                grad_dtype=torch.bfloat16, route="auto"):
+                                grad_dtype=torch.bfloat16, route="auto", plan="auto"):
         """K2 with the lm_head folded in (loss side): the policy's last hidden
         states [B, T, H] and lm_head weight [V, H] (bf16, H in LOSS_FROM_HIDDEN_SIZES) replace
         the logits — the reference's policy forward + logprobs_from_logits + PPO loss +
@@ -697,24 +742,17 @@ class PPOHotPath:
         route: "fused" (the kernels above; H in LOSS_FROM_HIDDEN_SIZES), "gemm" (the
         reference's own structure on the hot path's kernels: hipBLASLt bf16 logits -> the fused
         loss rows (policy_loss) -> hipBLASLt dh = dlogits·W and dW = dlogitsᵀ·h; any H, the
-        [B, T, V] logits and dlogits in HBM), "auto" = fused where it is built, else gemm."""
+        [B, T, V] logits and dlogits in HBM), "auto" = fused where it is built, else gemm.
+        plan (fused route): the dW pass's plan — "saved_p" (the forward's bf16 P tiles kept in
+        the workspace, ~2·N·V bytes = the size of bf16 logits, 0.62 GB at C2: 3 MFMA passes),
+        "recompute" (no N·V buffer: S recomputed in the dW pass, 4 passes), "auto" = saved_p
+        unless that workspace cannot be allocated (then recompute, until
+        release_loss_workspace())."""
         B, T, V = self.B, self.T, self.V
-        if hidden.dim() != 3 or tuple(hidden.shape[:2]) != (B, T) or weight.dim() != 2 or weight.shape[0] != V or \
-                weight.shape[1] != hidden.shape[2] or hidden.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
-            raise ValueError(f"hidden {tuple(hidden.shape)}/{hidden.dtype} and weight {tuple(weight.shape)}/"
-                             f"{weight.dtype} do not match the hot path ({B},{T},H) x ({V},H) bf16")
+        route = self._loss_from_hidden_route(hidden, weight, grad_dtype, route, plan)
         H = hidden.shape[2]
-        if grad_dtype not in (torch.bfloat16, torch.float32):
-            raise ValueError("grad_dtype must be bf16 or fp32")
-        if route not in ("auto", "fused", "gemm"):
-            raise ValueError(f"route must be auto, fused or gemm, not {route!r}")
-        if route == "auto":
-            route = "fused" if H in self.LOSS_FROM_HIDDEN_SIZES else "gemm"
         if route == "gemm":
             return self._policy_loss_from_hidden_gemm(hidden, weight, labels, values, old_values, mask, grad_dtype)
-        if H not in self.LOSS_FROM_HIDDEN_SIZES:
-            raise ValueError(f"policy_loss_from_hidden: fused route not built for hidden size {H} "
-                             f"{self.LOSS_FROM_HIDDEN_SIZES} (route='gemm' takes any H)")
         _lib.require_cuda(hidden, weight)
         labels = self._int64(labels, (B, T), "labels")
         mask = self._int64(mask, (B, T), "mask", required=False)
@@ -729,11 +767,9 @@ class PPOHotPath:
         if getattr(self, "dhidden", None) is None or self.dhidden.shape != (B, T, H) or self.dhidden.dtype != grad_dtype:
             self.dhidden = torch.empty((B, T, H), dtype=grad_dtype, device=self.device)
             self.dweight = torch.empty((V, H), dtype=grad_dtype, device=self.device)
-        # the saved-P plan's workspace (the forward's bf16 P tiles: ~V·N·2 bytes, 0.62 GB at C2);
-        # release_loss_workspace() frees it
-        nbytes = _lib.query("trlx_ppo_loss_from_hidden_workspace_bytes", N, H, V)
-        if getattr(self, "lm_loss_ws", None) is None or self.lm_loss_ws.numel() < nbytes:
-            self.lm_loss_ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        # the saved-P plan's workspace (the forward's bf16 P tiles: ~V·N·2 bytes, 0.62 GB at C2)
+        # or the recompute plan's; release_loss_workspace() frees it
+        lm_ws, lm_bytes = self._loss_workspace(N, H, V, plan)
         s = torch.cuda.current_stream(self.device)
         self._launch_pending_tail(s)
         if self.tail_done is not None:
@@ -743,8 +779,7 @@ class PPOHotPath:
                 _lib.dtype_code(old_values))
         outs = (float(self.cfg.cliprange), float(self.cfg.cliprange_value), float(self.cfg.vf_coef),
                 self.lp_new.data_ptr(), dh.data_ptr(), H, _lib.dtype_code(dh), dw.data_ptr(), _lib.dtype_code(dw), H,
-                self.dvalues.data_ptr(), self.workspace.data_ptr(), self.lm_loss_ws.data_ptr(),
-                self.lm_loss_ws.numel(), s.cuda_stream)
+                self.dvalues.data_ptr(), self.workspace.data_ptr(), lm_ws.data_ptr(), lm_bytes, s.cuda_stream)
         self._ev("loss", s)
         if self._split_mode:
             # split beta (the pipelined DP schedule, or step() with split_beta=True): the
@@ -813,8 +848,10 @@ class PPOHotPath:
         self.loss_logits = None
 
     def release_loss_workspace(self):
-        """Free the fused policy_loss_from_hidden workspace (its saved P tiles; re-allocated on next use)."""
+        """Free the fused policy_loss_from_hidden workspace (its saved P tiles; re-allocated on
+        next use, when plan "auto" tries the saved-P plan's size again)."""
         self.lm_loss_ws = None
+        self._loss_ws_fallback = False
 
     def release_lm_logits(self):
         """Free the gemm route's [2, chunk, T, V] logits ring (re-allocated on next use)."""
@@ -897,20 +934,27 @@ class PPOHotPath:
         noise, and no launch of it can host the rollout waves."""
         self._check_hidden(hidden, weight, ref_hidden, ref_weight)
         w_new = weight if new_weight is None else new_weight
-        if tuple(new_hidden.shape[:2]) != (self.B, self.T) or new_hidden.dim() != 3:
-            raise ValueError(f"new_hidden {tuple(new_hidden.shape)} does not match ({self.B},{self.T},H)")
+        # the loss side's checks now, before any launch of this batch (a failure inside the next
+        # call's loss would lose this batch after its experience had run)
+        loss_route = self._loss_from_hidden_route(new_hidden, w_new, grad_dtype, loss_route)
         route = self._lm_route(route, hidden, ref_hidden)
 
         def experience(labels, lengths, s):
             self._experience_lmhead(hidden, weight, ref_hidden, ref_weight, labels, lengths, s, route)
 
         def loss(p, fold):
+            # batch k's loss runs in call k+1: its lm_head weight must still be the one it was
+            # submitted with (an in-place optimizer.step in between would pair hidden(k) with W(k+1))
+            if p["new_weight"]._version != p["weight_version"]:
+                raise RuntimeError("pipeline_step_from_hidden: new_weight was modified in place between the call "
+                                   "that submitted the batch and the one running its loss; step the optimizer "
+                                   "after pipeline_flush(), or pass a copy")
             return self.policy_loss_from_hidden(p["new_hidden"], p["new_weight"], p["labels"], p["values"],
                                                 p["old_values"], mask=p["mask"], grad_dtype=p["grad_dtype"],
                                                 route=p["loss_route"])
 
         return self._pipeline(experience, loss, dict(new_hidden=new_hidden, new_weight=w_new, grad_dtype=grad_dtype,
-                                                     loss_route=loss_route),
+                                                     loss_route=loss_route, weight_version=w_new._version),
                               labels, old_values, values, scores, lengths, mask, group, fold=False)
 
     def _pipeline(self, experience, loss, payload, labels, old_values, values, scores, lengths, mask, group, fold):
