@@ -235,7 +235,9 @@ def test_lm_head_logprobs_split_plans(splits, tsplit):
     torch.testing.assert_close(got[0].double(), lp64, rtol=1e-5, atol=2e-5)
     assert _rel(got[1], dh64) < 1e-2 and _rel(got[2], dw64) < 1e-2
     torch.testing.assert_close(got[0], base[0], rtol=1e-6, atol=1e-5)
-    assert _rel(got[1], base[1]) < 2e-3 and _rel(got[2], base[2]) < 2e-3
+    # dW: the split plan sets the per-split scale e' of the saved-P plan's scaled rows
+    # hq = −g·e'·h, so their bf16 rounding differs between plans (two roundings apart)
+    assert _rel(got[1], base[1]) < 2e-3 and _rel(got[2], base[2]) < 6e-3
 
 
 def test_loss_from_hidden_gemm_route_matches_fused():

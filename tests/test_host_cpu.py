@@ -233,16 +233,17 @@ def test_tuning_rejects_removed_forms_and_restores():
 
 def test_savep_region_sizes():
     """The saved-P region of the drop-in pair: the P tiles (⌈V/64⌉ x 2⌈N/64⌉ x 4 KB, the size of
-    bf16 logits rounded to tiles) + 8 records of 16 B per token; the PPO entries' saved-P
-    workspace holds the same on top of the recompute plan's."""
+    bf16 logits rounded to tiles) + 8 fp32 split scales per token; the PPO entries' saved-P
+    workspace holds the P tiles and the per-split scaled h rows (8·N·H bf16) on top of the
+    recompute plan's."""
     import trlx_t5_amd as P
     q = P._lib.query
     N, H, V = 6144, 768, 50257
     pbytes = ((V + 63) // 64) * 2 * ((N + 63) // 64) * 4096
-    assert q("trlx_lmhead_savep_bytes", N, H, V) == pbytes + 8 * N * 16
+    assert q("trlx_lmhead_savep_bytes", N, H, V) == pbytes + 8 * N * 4
     assert pbytes >= 2 * N * V
     big, small = q("trlx_ppo_loss_from_hidden_workspace_bytes", N, H, V), q("trlx_lmhead_loss_workspace_bytes", N, H, V)
-    assert big - small >= pbytes + 8 * N * 16
+    assert big - small >= pbytes + 8 * N * H * 2
     assert q("trlx_ppo_loss_from_hidden_plan", N, H, V, big) == 1
     assert q("trlx_ppo_loss_from_hidden_plan", N, H, V, small) == 0
 

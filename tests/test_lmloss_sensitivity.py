@@ -21,9 +21,12 @@ def _bf(x):
     return x.to(torch.bfloat16).double()
 
 
-def _emulate(h, w, y, g, mutate=None, out_bf16=True):
+def _emulate(h, w, y, g, mutate=None, out_bf16=True, plan="recompute"):
     """The kernels' arithmetic (fp32 products of bf16 operands, bf16 P / dS), with an optional
-    mutation.  Returns (E, dh, dW) in fp64 holding the emulated values."""
+    mutation.  Returns (E, dh, dW) in fp64 holding the emulated values.  plan "saved_p": dW as
+    k_lmloss_dwp forms it (one vocab split here): the forward's bf16 P = exp(S − m) with each
+    token's label entry replaced by bf16(−(1 − p_y)/e'), times the bf16 scaled rows
+    hq = −g·e'·h, e' = e^(m − lse)."""
     hf, wf = h.float(), w.float()
     s = hf @ wf.t()                                    # fp32 MFMA accumulation
     m = s.max(-1, keepdim=True).values                  # the forward's exponent offset
@@ -41,9 +44,17 @@ def _emulate(h, w, y, g, mutate=None, out_bf16=True):
     lse = m + torch.log(l)
     p = torch.exp(s - lse)                              # the dW kernel's recomputed p
     k = {"pw_zero": 0.0, "pw_x0.9": 0.9}.get(mutate, 1.0)
-    ds = -g[:, None] * p * k
-    ds[torch.arange(len(y)), y] += g
-    dw = (_bf(ds).t() @ hf.double()).float()
+    if plan == "saved_p":
+        ep = torch.exp(m - lse)                          # e' (one split: m is the split's offset)
+        a_op = pf * k
+        py = p[torch.arange(len(y)), y]
+        a_op[torch.arange(len(y)), y] = -(1.0 - py) / ep[:, 0]
+        hq = -g[:, None] * ep * hf
+        dw = (_bf(a_op).t() @ _bf(hq)).float()
+    else:
+        ds = -g[:, None] * p * k
+        ds[torch.arange(len(y)), y] += g
+        dw = (_bf(ds).t() @ hf.double()).float()
     if mutate == "tail_block_zero":
         V = w.shape[0]
         dw[(V // 64) * 64:] = 0.0
@@ -62,9 +73,9 @@ def _operands(kind, N, H, V, seed):
     return C.peaked_operands(N, H, V, seed, wscale=3.3 / H ** 0.5)
 
 
-def _errors(h, w, y, g, mutate, out_bf16):
+def _errors(h, w, y, g, mutate, out_bf16, plan="recompute"):
     t = C.fp64_truth(h, w, y, g)
-    e, dh, dw = _emulate(h, w, y, g.float(), mutate, out_bf16)
+    e, dh, dw = _emulate(h, w, y, g.float(), mutate, out_bf16, plan)
     errs = C.e_errors(e, t["e"])
     errs.update(C.dw_errors(dw, t["dw"], y))
     errs.update(C.dh_errors(dh, t["dh"], g, t["e"], fp32_out=not out_bf16))
@@ -76,10 +87,11 @@ CASES = [("flat", 256, 128, 3000), ("peaked", 256, 128, 3000), ("flat", 96, 64, 
 
 @pytest.mark.parametrize("kind,N,H,V", CASES)
 @pytest.mark.parametrize("out_bf16", [True, False])
-def test_checks_pass_the_kernels_arithmetic(kind, N, H, V, out_bf16):
+@pytest.mark.parametrize("plan", ["recompute", "saved_p"])
+def test_checks_pass_the_kernels_arithmetic(kind, N, H, V, out_bf16, plan):
     h, w, y = _operands(kind, N, H, V, N + V)
     g = torch.randn(N, generator=torch.Generator().manual_seed(1))
-    errs = _errors(h, w, y, g, None, out_bf16)
+    errs = _errors(h, w, y, g, None, out_bf16, plan)
     C.assert_within(errs, f"emulated kernels, {kind}")
     # the margin is real: the emulation sits well inside every limit
     assert all(v < 0.6 * C.LIMITS[k] for k, v in errs.items()), errs

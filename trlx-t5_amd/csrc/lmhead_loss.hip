@@ -119,13 +119,14 @@ struct LmLossArgs {
     int dw_vpw;      // vocab rows per dW workgroup (64; the saved-P plan's RW = 2 form: 128)
     float* dwpart;
     // saved-P plan (k_lmloss_dwp): the forward stores its bf16 P tiles in the dW kernel's layout
-    // (ll_p_save), the combine a per-(split, token) record {g·e^(m_split − lse), g·(1 − p_y), y, 0}
+    // (ll_p_store); the combine overwrites each token's label entry with −(1 − p_y)/e' and writes
+    // the token's h row scaled per split, hq = −g·e'·h with e' = e^(m_split − lse), so dW = P·hq
+    // with no per-element arithmetic in the dW kernel (ll_scale)
     uint16_t* pbuf;  // NULL = the recompute plan (k_lmloss_dw)
     int pntt;        // 32-token tiles of the P layout (2·⌈N / 64⌉)
-    f32x4_t* prec;   // [kLLMaxSplits][N] (compact token index)
-    // the drop-in pair (kLLFwd with pbuf: the combine writes g-free records {e^(m_split − lse),
-    // 1 − p_y, y, 0} to prec; kLLBwd: reads them here and writes the g-scaled ones to prec)
-    const f32x4_t* psrc;
+    uint16_t* hq;    // [kLLMaxSplits][N][H] bf16, compact token index (the combine with g: kLLPpo / kLLBwd)
+    float* erec;     // [kLLMaxSplits][N] e' per (split, compact token): the drop-in forward writes, its
+                     // backward reads (the saved region)
     int ncu;         // compute units (the forward's split choice, ll_fwd_splits)
     int mode;
     // ---- per-token PPO fields (the names ppo_token.h reads; see RowArgs in vocab_rows.hip)
@@ -322,6 +323,30 @@ __device__ __forceinline__ int ll_fwd_splits(const LmLossArgs& a, int ntb) {
     return best;
 }
 
+// Vocab tiles of split s: [ll_split_t0(s), ll_split_t0(s + 1)), whole 4-tile (128-row) granules,
+// so a saved-P dW workgroup's 128 vocab rows never straddle two splits (its four waves share one
+// staged tile of the split's scaled h); the largest split is at most 3 tiles over the even share.
+__device__ __forceinline__ int ll_split_t0(int s, int nvt, int nsplit) {
+    return min(nvt, 4 * int(int64_t(s) * ((nvt + 3) >> 2) / nsplit));
+}
+__device__ __forceinline__ int ll_split_of(int vt, int nvt, int nsplit) {
+    int s = 0;
+    for (int k = 1; k < nsplit; ++k) s = ll_split_t0(k, nvt, nsplit) <= vt ? k : s;
+    return s;
+}
+// The scale of split s's P for a token: e' = e^(m_s − lse) (a split with no vocab: 0), clamped to
+// 2^-100 from below so the label entry −(1 − p_y)/e' stays finite (terms of a split whose
+// e^(m_s − lse) underflows are then weighted by 2^-100 instead of less: below any fp32 gradient)
+__device__ __forceinline__ float ll_scale(float ms, float lse) {
+    return ms == -INFINITY ? 0.0f : fmaxf(exp2_fast((ms - lse) * kLog2e), 0x1p-100f);
+}
+// P[vocab row v][compact token m] in the saved-P layout (ll_p_store)
+__device__ __forceinline__ uint16_t* ll_p_elem(const LmLossArgs& a, int v, int m) {
+    const int vt = v >> 5, rr = v & 31, j32 = m & 31;
+    return a.pbuf + (((int64_t(vt >> 1) * a.pntt + (m >> 5)) * 4 + 2 * (vt & 1) + (rr >> 4)) * 1024 +
+                     16 * (16 * (j32 >> 3) + (rr & 15)) + 2 * (j32 & 7)) / 2;
+}
+
 // ------------------------------------------------------------------ forward, 16x16x32 form
 // A workgroup = 64 tokens (four blocks of 16, one softmax per wave: block w) x one vocab split;
 // h fragments 96 registers, O 192 at H = 768.  Without the two splits below (LL_FWD_SPAIR,
@@ -447,7 +472,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     const char* sxr = smem + 3 * kStage + (wave ^ 1) * 4096 + 16 * (lane & 63);
     char* sxw = pscr + 16 * (lane & 63);
     const int nvt = (a.V + kLLRows - 1) / kLLRows;
-    const int t0 = int(int64_t(split) * nvt / nsplit), t1 = int(int64_t(split + 1) * nvt / nsplit);
+    const int t0 = ll_split_t0(split, nvt, nsplit), t1 = ll_split_t0(split + 1, nvt, nsplit);
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
     auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
@@ -884,17 +909,28 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
         lse = M + lsum;
         e *= 1.0f / L;
         const float lp = yok ? (xlab - M) - lsum : NAN;  // the reference's order, as in the rows
+        // the saved-P plan: the split scales e' and the label entry of P (ll_scale)
+        float es[kLLMaxSplits];
+#pragma unroll
+        for (int s = 0; s < kLLMaxSplits; ++s) es[s] = s < nsplit ? ll_scale(ml[s].x, lse) : 0.0f;
+        if (a.pbuf && d4 == 0 && yok) {
+            const int nvt = (a.V + kLLRows - 1) / kLLRows, sy = ll_split_of(int(y) >> 5, nvt, nsplit);
+            float ey = es[0];
+#pragma unroll
+            for (int s = 1; s < kLLMaxSplits; ++s) ey = sy == s ? es[s] : ey;
+            *ll_p_elem(a, int(y), m) = f2bf(expm1f(lp) / ey);  // −(1 − p_y)/e'
+        }
         if (MODE == kLLPpo) {
             PolicyTerms pt;
             g = ppo_policy_dlp(lp, p.olp, p.A, p.m, p.inv_msum, a.cliprange, pt);
-            if (a.prec && d4 < nsplit) {
-                // the saved-P plan: split d4's record, dS = (y == v) ? g·(1 − p_y) : −g·e^(m_s − lse)·P
-                float ms = ml[0].x;
+            if (a.hq) {  // the token's h scaled per split: hq = −g·e'·h
 #pragma unroll
-                for (int s = 1; s < kLLMaxSplits; ++s) ms = d4 == s ? ml[s].x : ms;
-                const float q = ms == -INFINITY ? 0.0f : g * exp2_fast((ms - lse) * kLog2e);
-                const float dlab = fmaf(-g, exp2_fast(lp * kLog2e), g);
-                a.prec[int64_t(d4) * a.N + m] = f32x4_t{q, dlab, __int_as_float(yok ? int(y) : -1), 0.0f};
+                for (int s = 0; s < kLLMaxSplits; ++s) {
+                    if (s >= nsplit) break;
+                    const float q = -g * es[s];
+                    reinterpret_cast<uint2*>(a.hq + (int64_t(s) * a.N + m) * a.H)[d4] =
+                        make_uint2(pack_bf2(q * bf_lo(hv.x), q * bf_hi(hv.x)), pack_bf2(q * bf_lo(hv.y), q * bf_hi(hv.y)));
+                }
             }
             if (d4 == 0) {
                 const bool masked = p.m == 0.0f;
@@ -904,13 +940,11 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
                 if (a.coef || a.wstats) split_outputs(a, row, p);
             }
         } else {  // kLLFwd
-            if (a.prec && d4 < nsplit) {  // the drop-in's saved-P records, without g (the backward's)
-                float ms = ml[0].x;
+            if (a.erec && d4 < nsplit) {  // the drop-in: e' kept for the backward (which knows g)
+                float ed = es[0];
 #pragma unroll
-                for (int s = 1; s < kLLMaxSplits; ++s) ms = d4 == s ? ml[s].x : ms;
-                const float q = ms == -INFINITY ? 0.0f : exp2_fast((ms - lse) * kLog2e);
-                const float dlab = 1.0f - exp2_fast(lp * kLog2e);
-                a.prec[int64_t(d4) * a.N + m] = f32x4_t{q, dlab, __int_as_float(yok ? int(y) : -1), 0.0f};
+                for (int s = 1; s < kLLMaxSplits; ++s) ed = d4 == s ? es[s] : ed;
+                a.erec[int64_t(d4) * a.N + m] = ed;
             }
             if (d4 == 0) {
                 st_any(a.lp, a.lp_dtype, row, lp);
@@ -921,11 +955,15 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
         e = reinterpret_cast<const f32x4_t*>(a.ebuf + int64_t(row) * a.H)[d4];
         lse = a.lse_io[row];
         g = ld_any(a.gin, a.gin_dtype, row);
-        if (a.psrc && d4 < kLLMaxSplits) {  // the saved-P plan: the forward's records scaled by g
+        if (a.hq) {  // the saved-P plan: hq = −g·e'·h from the forward's e'
             nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
-            if (d4 < nsplit) {
-                const f32x4_t r = a.psrc[int64_t(d4) * a.N + m];
-                a.prec[int64_t(d4) * a.N + m] = f32x4_t{g * r.x, g * r.y, r.z, 0.0f};
+            const uint2 hv = reinterpret_cast<const uint2*>(a.h + int64_t(row) * a.ldh)[d4];
+#pragma unroll
+            for (int s = 0; s < kLLMaxSplits; ++s) {
+                if (s >= nsplit) break;
+                const float q = -g * a.erec[int64_t(s) * a.N + m];
+                reinterpret_cast<uint2*>(a.hq + (int64_t(s) * a.N + m) * a.H)[d4] =
+                    make_uint2(pack_bf2(q * bf_lo(hv.x), q * bf_hi(hv.x)), pack_bf2(q * bf_lo(hv.y), q * bf_hi(hv.y)));
             }
         }
     }
@@ -1167,23 +1205,24 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
 }
 
 // ------------------------------------------------------------------ dW from the saved P
-// k_lmloss_dw without its Sᵀ pass: the forward left every bf16 P tile in HBM in this kernel's
-// A-operand layout (ll_p_stage / ll_p_store) and the combine a record per (split, token)
-// {q = g·e^(m_split − lse), dlab = g·(1 − p_y), y}, so dS = (y == v) ? dlab : −q·P — the P of the
-// E product rescaled to the final lse, the label entry from the fp32 label logit.  Workgroup =
-// 64·RW vocab rows (4 waves x 16·RW rows over the whole H; dW accumulators 192·RW registers at
-// H = 768) x one token split; per 32-token tile ONE product, dW += dS·h_tile (RW x H/16 MFMAs
-// v_mfma_f32_16x16x32_bf16; the h tile read transposed, each fragment feeding RW MFMAs: lane
-// group g's k slots = tokens 8g..8g+7, rows 8g + q and 8g + 4 + q of the subtile image —
-// conflict-free on the ll16_swz image).  RW = 2 halves the h bytes staged and read from LDS per
-// MFMA (the RW = 1 form's dW phase ran at ~2.7x its MFMA time, bound by the DMA issue and the
-// LDS reads).  The dS of the NEXT tile is formed in the MFMA gaps (records read in two groups
-// of 4, the values after them).  Loads run ahead: a 3-stage h ring (the DMA of tile t+2 during
-// tile t), 3 record slots (tile t+3), P chunks in 3 register sets (tile t+3's load issued at
-// tile t), and the barrier waits only for what was issued before the previous tile (counted
-// vmcnt: P streams from HBM, 0.62 GB per call at C2).
+// dW = Σ_t dS_t·h_t with dS = (y == v) ? g·(1 − p_y) : −g·e^(m_split − lse)·P, regrouped so the
+// dW kernel does no arithmetic on its operands: the forward left every bf16 P tile in HBM in this
+// kernel's A-operand layout (ll_p_store), the combine overwrote each token's label entry with
+// −(1 − p_y)/e' and wrote the token's h row scaled per vocab split, hq_s = −g·e'_s·h (e' =
+// e^(m_s − lse), ll_scale), so
+//   dW[v] = Σ_t P[v][t] · hq_{split(v)}[t]          (label entries: −(1 − p_y)/e' · −g·e'·h = g·(1 − p_y)·h)
+// — ONE plain MFMA product per 32-token tile: the A operand is the P chunk as loaded (one 16-B
+// load a lane, three tiles ahead), the B operand the staged hq tile read transposed.  Numerics as
+// the per-element form it replaced (round 5: dS formed from P and a per-(split, token) record in
+// the MFMA gaps, ~430 of its 1,910 cycles a tile): one bf16 rounding on each side of every product
+// (P, and hq instead of dS).  Workgroup = 64·RW vocab rows (4 waves x 16·RW rows; HSP = 2: half the
+// hidden columns, the two halves adjacent in dispatch order so the second P read hits the
+// Infinity Cache) x one token split; its rows lie in one vocab split (ll_split_t0's 128-row
+// granules), so the four waves share each staged hq tile.  3-stage hq ring (the DMA of tile t+2
+// during tile t) and counted vmcnt: the barrier waits only for what was issued before the
+// previous tile.
 #ifndef LL_DWP_PFO
-#define LL_DWP_PFO 8  // transposed h fragments in flight
+#define LL_DWP_PFO 8  // transposed hq fragments in flight
 #endif
 #ifndef LL_DWP_PIECE_GAP
 #define LL_DWP_PIECE_GAP 4
@@ -1193,25 +1232,17 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
 #endif
 template <class G, int RW, int HSP>
 __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
-    // HSP = 2: a workgroup owns HALF the hidden columns of its vocab rows (h part hp = blockIdx
-    // & 1, the two parts of a block adjacent in dispatch order so the second P read hits the
-    // Infinity Cache): RW = 2 then holds 32 rows x H/2 = 192 accumulators, the RW = 1 budget
     constexpr int H = G::H, HC = H / HSP, DB = HC / 16, NI = G::NI / HSP;
     constexpr int kStage = G::kStage / HSP;
-    constexpr int kRecSlot = RW == 1 ? 1024 : 4096;  // RW = 2: each wave's own 1-KB records
     static_assert(G::kWaves == 4, "dW: four waves per workgroup");
     static_assert(HC % 128 == 0, "h parts of whole 128-column segments");
-    static_assert(3 * kStage + 3 * kRecSlot <= 163840, "3 h stages + 3 record slots");
-    // the next-but-one tile's h pieces every kPG-th gap from kPO on
+    static_assert(3 * kStage <= 163840, "3 hq stages");
+    // the next-but-one tile's hq pieces every kPG-th gap from kPO on
     constexpr int kPG = LL_DWP_PIECE_GAP, kPO = LL_DWP_PIECE_OFF;
     static_assert(kPO < kPG && kPG * (NI - 1) + kPO < DB, "every DMA piece inside the tile's gaps");
-    // + each wave's RW KB of dS hand-off (below)
-    static_assert(3 * kStage + 3 * kRecSlot + 4096 * RW <= 163840, "LDS budget with the dS hand-off");
-    __shared__ __attribute__((aligned(16))) char smem[3 * kStage + 3 * kRecSlot + 4096 * RW];
-    char* recs = smem + 3 * kStage;
+    __shared__ __attribute__((aligned(16))) char smem[3 * kStage];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    char* dsl = recs + 3 * kRecSlot + 1024 * RW * wave + 16 * lane;
     const int g = lane >> 4, c = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
     const int nv = a.rows ? *a.nrows : a.N;
     constexpr int vpw = 64 * RW;
@@ -1223,19 +1254,10 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     const int r0 = vb * vpw + wave * 16 * RW;  // this wave's first vocab row
     const int ntt = (nv + kLLRows - 1) / kLLRows;
     const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
-    // the forward's split of the vocab tiles (ll_fwd_splits: the same plan)
+    // the vocab split of the workgroup's rows (the forward's plan, ll_fwd_splits / ll_split_t0)
     const int nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
-    const int nvt = (a.V + kLLRows - 1) / kLLRows;
-    auto split_of = [&](int vt) {
-        int s = 0;
-        for (int k = 1; k < nsplit; ++k) s = int(int64_t(k) * nvt / nsplit) <= vt ? k : s;
-        return s;
-    };
-    // the records this lane DMAs and where the wave reads its tokens' records (+ 16·j)
-    const int srec = RW == 1 ? split_of(2 * vb + (lane >> 5)) : split_of(4 * vb + wave);
-    const int rdst = RW == 1 ? 0 : 1024 * wave;
-    const int rb16 = (RW == 1 ? 512 * (wave >> 1) : 1024 * wave) + 16 * (8 * g);
-    // transposed reads of the h tile: rows 8g + 4hf + q, columns 16nb + 4p (the subtile image)
+    const int sp = ll_split_of((vb * vpw) >> 5, (a.V + kLLRows - 1) / kLLRows, nsplit);
+    // transposed reads of the hq tile: rows 8g + 4hf + q, columns 16nb + 4p (the subtile image)
     int trb8[2][2];
 #pragma unroll
     for (int par = 0; par < 2; ++par)
@@ -1251,32 +1273,18 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
         const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         return __builtin_bit_cast(bf16x8_t, v);
     };
-    auto tok_row = [&](int m) { return m < nv ? (a.rows ? a.rows[m] : m) : a.N; };
-    const int rA = ll_piece_row(wave, lane), rB = ll_piece_row(wave + G::kWaves, lane);
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.h, uint32_t(int64_t(a.N) * a.ldh * 2));
-    const __amdgpu_buffer_rsrc_t rrec = make_rsrc(a.prec, uint32_t(kLLMaxSplits) * uint32_t(a.N) * 16u);
-    const __amdgpu_buffer_rsrc_t rrows = make_rsrc(a.rows, a.rows ? uint32_t(a.N) * 4u : 0u);
+    // hq rows [nsplit][N][H]: the host keeps nsplit·N·H·2 below the 2 GB sentinel (ll_hq_fits)
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.hq, uint32_t(int64_t(nsplit) * a.N * H * 2));
+    const int hrow0 = sp * a.N;  // hq row of compact token 0 of this split
     auto stage = [&](int t) __attribute__((always_inline)) { return smem + (t % 3) * kStage; };
-    auto rslot = [&](int t) __attribute__((always_inline)) { return recs + (t % 3) * kRecSlot; };
     // piece il of the part's image = piece hp·HC/16 + il of the full-H image (a multiple of 8:
-    // the same rows)
-    auto issue_piece = [&](int t, char* slot, int k, int ra, int rbw) __attribute__((always_inline)) {
+    // the same rows); tokens past the live count read as zero rows (out of range)
+    auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
         const int il = wave + G::kWaves * k, i = hp * (HC / 16) + il;
-        const int rbytes = int(__umul24(uint32_t(((il & 7) == (wave & 7)) ? ra : rbw), uint32_t(a.ldh) * 2u));
-        const int off = ll16_piece_src(i, rbytes, lane);
+        const int m = t * kLLRows + ll_piece_row(il, lane);
+        const int off = ll16_piece_src(i, (hrow0 + m) * (H * 2), lane);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + il * 1024), 16,
-                                                 t < t1 ? off : int(0x7ffff000), 0, 0, 0);
-    };
-    // records of tile t: lane l -> split srec, token t·32 + (l & 31), at byte rdst + 16·l of the
-    // slot (RW = 1: lanes 32-63 the block's second vocab tile, every wave the same DMA; RW = 2:
-    // each wave its own tile's, lanes 32-63 a copy); zero past the live tokens (q = dlab = 0:
-    // dS = 0 whatever P holds there).  No wave-dependent branch: every wave's count of loads in
-    // flight is the same and the counted waits stay exact.
-    auto issue_recs = [&](int t, char* slot) __attribute__((always_inline)) {
-        const int m = t * kLLRows + (lane & 31);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rrec, (__attribute__((address_space(3))) void*)(slot + rdst), 16,
-                                                 t < t1 && m < nv ? (srec * a.N + m) * 16 : int(0x7ffffff0), 0, 0,
-                                                 0);
+                                                 t < t1 && m < nv ? off : int(0x7ffff000), 0, 0, 0);
     };
     // P chunk of tile t for row half hh (rows r0 + 16hh + c, tokens 8g..8g+7), clamped to the
     // split's last tile: 64-row block (r0 + 16hh) / 64, dW wave slot ((r0 + 16hh) / 16) & 3
@@ -1290,31 +1298,15 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     auto load_p = [&](int t, int hh) __attribute__((always_inline)) {
         return pbase[hh][int64_t(min(t, t1 - 1)) * 256];
     };
-    auto ds_of = [&](const f32x4_t& rec, short pe, int vcol) __attribute__((always_inline)) {
-        const float pv = __uint_as_float(uint32_t(uint16_t(pe)) << 16);
-        return __float_as_int(rec.z) == vcol ? rec.y : -rec.x * pv;
-    };
-    auto rec_at = [&](const char* slot, int e) __attribute__((always_inline)) {
-        return *reinterpret_cast<const f32x4_t*>(slot + rb16 + 16 * e);
-    };
     f32x4_t D[RW][DB];  // dW[r0 + 16hh + 4g + r][16nb + c]
 #pragma unroll
     for (int hh = 0; hh < RW; ++hh)
 #pragma unroll
         for (int nb = 0; nb < DB; ++nb) D[hh][nb] = f32x4_t{};
-    bf16x8_t da[RW];
-    s16x8_t R0[RW], R1[RW], R2[RW];  // P(t0 + k) in R[k % 3]
+    s16x8_t R0[RW], R1[RW], R2[RW], R3[RW];  // P(t0 + k) in R[k % 4]
 #pragma unroll
-    for (int hh = 0; hh < RW; ++hh) {
-        da[hh] = bf16x8_t{};
-        R0[hh] = R1[hh] = R2[hh] = s16x8_t{};
-    }
-    int nrowA = 0, nrowB = 0;  // rows of tile t+2 at the start of tile t
+    for (int hh = 0; hh < RW; ++hh) R0[hh] = R1[hh] = R2[hh] = R3[hh] = s16x8_t{};
     if (t0 < t1) {
-        const int rowA0 = tok_row(t0 * kLLRows + rA), rowB0 = tok_row(t0 * kLLRows + rB);
-        const int rowA1 = tok_row((t0 + 1) * kLLRows + rA), rowB1 = tok_row((t0 + 1) * kLLRows + rB);
-        nrowA = a.rows ? a.rows[min((t0 + 2) * kLLRows + rA, nv - 1)] : 0;
-        nrowB = a.rows ? a.rows[min((t0 + 2) * kLLRows + rB, nv - 1)] : 0;
 #pragma unroll
         for (int hh = 0; hh < RW; ++hh) {
             R0[hh] = load_p(t0, hh);
@@ -1322,53 +1314,21 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
             R2[hh] = load_p(t0 + 2, hh);
         }
 #pragma unroll
-        for (int k = 0; k < NI; ++k) issue_piece(t0, stage(t0), k, rowA0, rowB0);
+        for (int k = 0; k < NI; ++k) issue_piece(t0, stage(t0), k);
 #pragma unroll
-        for (int k = 0; k < NI; ++k) issue_piece(t0 + 1, stage(t0 + 1), k, rowA1, rowB1);
-        issue_recs(t0, rslot(t0));
-        issue_recs(t0 + 1, rslot(t0 + 1));
-        issue_recs(t0 + 2, rslot(t0 + 2));
+        for (int k = 0; k < NI; ++k) issue_piece(t0 + 1, stage(t0 + 1), k);
         __builtin_amdgcn_s_waitcnt(ll_vmcnt(0));
         ll_lds_barrier();
-#pragma unroll
-        for (int hh = 0; hh < RW; ++hh) {
-            float ds[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ds[e] = ds_of(rec_at(rslot(t0), e), R0[hh][e], r0 + 16 * hh + c);
-            da[hh] = pack8(ds);
-        }
     }
-#if LL_STAMP
-    unsigned long long stamp[8] = {};
-#endif
-    // tile t: dW(t) with da = dS(t); in its gaps the loads of the tiles ahead and dS(t+1) from
-    // puse = P(t+1) and the records of t+1 (rnx); pnew receives P(t+3).  The LDS regions are
-    // __restrict__ parameters (alias scopes: the DMA targets fut / rfut apart from the regions
-    // read, as k_lmloss_dw — without them hipcc waits for the DMA before every read).
-    auto tile_body = [&](const char* __restrict__ cur, char* __restrict__ fut, const char* __restrict__ rnx,
-                         char* __restrict__ rfut, int t, const s16x8_t (&puse)[RW], s16x8_t (&pnew)[RW])
-                         __attribute__((always_inline)) {
-        const int ma = (t + 2) * kLLRows + rA, mb1 = (t + 2) * kLLRows + rB;  // tile t+2's rows
-        const int pa = ma < nv ? (a.rows ? nrowA : ma) : a.N;
-        const int pb = mb1 < nv ? (a.rows ? nrowB : mb1) : a.N;
-        nrowA = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rA, nv - 1) * 4, 0, 0);
-        nrowB = __builtin_amdgcn_raw_buffer_load_b32(rrows, min((t + 3) * kLLRows + rB, nv - 1) * 4, 0, 0);
-        if (!(kLLAblate & 128)) {
+    // tile t: dW += P(t)·hq(t) with P(t) in `use`; in its gaps the DMA of tile t+2 (fut) and the
+    // P loads of tile t+3 (into `nw`).  The LDS regions are __restrict__ parameters (alias scopes:
+    // hipcc otherwise waits for the DMA before every read of the current tile).
+    auto tile_body = [&](const char* __restrict__ cur, char* __restrict__ fut, int t, const s16x8_t (&use)[RW],
+                         s16x8_t (&nw)[RW]) __attribute__((always_inline)) {
+        constexpr int PFO = LL_DWP_PFO;
+        bf16x8_t da[RW], tf[DB];
 #pragma unroll
-            for (int hh = 0; hh < RW; ++hh) pnew[hh] = load_p(t + 3, hh);
-        }
-        bf16x8_t dn[RW];
-        f32x4_t rr[8];
-        float dsn[RW][8];
-        // gaps: the 8 records read at kR (4 + 4), then one dS value per gap from kD on (L gaps
-        // ≈ 128 MFMA cycles later; one at a time, so the VALU work hides behind the MFMAs of
-        // its gap: four values in one gap had cost ~400 cycles a tile), the packs after them;
-        // transposed reads PFO fragments ahead (≈ 256 MFMA cycles)
-        constexpr int PFO = LL_DWP_PFO, L = 8 / RW, kR = 1, kD = kR + 1 + L;
-        constexpr int VPG = (8 * RW + (DB - kD - 2)) / (DB - kD - 1);  // dS values per gap
-        constexpr int kPk = kD + (8 * RW + VPG - 1) / VPG;
-        static_assert(kPk < DB, "the dS gaps");
-        bf16x8_t tf[DB];
+        for (int hh = 0; hh < RW; ++hh) da[hh] = __builtin_bit_cast(bf16x8_t, use[hh]);
 #pragma unroll
         for (int nb = 0; nb < PFO; ++nb) tf[nb] = tr_frag(cur, nb);
 #pragma unroll
@@ -1377,71 +1337,27 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
 #pragma unroll
             for (int hh = 0; hh < RW; ++hh)
                 D[hh][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[hh], tf[nb], D[hh][nb], 0, 0, 0);
-            // (the four waves' pieces in the same gaps: staggering them by wave — a wave-uniform
-            // branch per gap — measured slower in both kernels, the forward's S loop 2,033 ->
-            // 3,900 cycles a tile)
-            if (nb % kPG == kPO && nb / kPG < NI && !(kLLAblate & 256)) issue_piece(t + 2, fut, nb / kPG, pa, pb);
-            if (nb == 2) issue_recs(t + 3, rfut);
+            if (nb == 0) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (nb == kR) rr[e] = rec_at(rnx, e);
-                if (nb == kR + 1) rr[4 + e] = rec_at(rnx, 4 + e);
+                for (int hh = 0; hh < RW; ++hh) nw[hh] = load_p(t + 3, hh);
             }
-#pragma unroll
-            for (int hh = 0; hh < RW; ++hh) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (nb == kD + (RW * e + hh) / VPG) {
-                        dsn[hh][e] = ds_of(rr[e], puse[hh][e], r0 + 16 * hh + c);
-                        asm volatile("" : "+v"(dsn[hh][e]));  // formed in this gap, not sunk to the store
-                    }
-                // the next tile's A operand goes through the wave's LDS slot and is read back after
-                // this tile's last MFMA: handed over in registers (dn copied into da), hipcc gave
-                // both the same registers and sank the whole dS computation to after the last
-                // MFMA (~400 cycles a tile, serial; ISA); the store pins it to its gaps
-                if (nb == kPk) {
-                    *reinterpret_cast<bf16x8_t*>(dsl + 1024 * hh) = pack8(dsn[hh]);
-                    asm volatile("" ::: "memory");
-                }
-            }
-            if (nb == DB - 1) {
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int hh = 0; hh < RW; ++hh) dn[hh] = *reinterpret_cast<const bf16x8_t*>(dsl + 1024 * hh);
-            }
+            if (nb % kPG == kPO && nb / kPG < NI) issue_piece(t + 2, fut, nb / kPG);
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (!(kLLAblate & 512)) {
-#pragma unroll
-            for (int hh = 0; hh < RW; ++hh) da[hh] = dn[hh];
-        }
     };
-    auto tile = [&](int t, const s16x8_t (&puse)[RW], s16x8_t (&pnew)[RW]) __attribute__((always_inline)) {
-        unsigned long long ts0 = 0, ts1 = 0, ts2 = 0;
-        LL_TS(ts0);
-        // everything issued before the previous tile (2 row indices, RW P chunks, NI pieces, the
-        // records: NI + 3 + RW per tile): h(t), the records and P of t+1
-        __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI + 3 + RW));
+    auto tile = [&](int t, const s16x8_t (&use)[RW], s16x8_t (&nw)[RW]) __attribute__((always_inline)) {
+        // everything issued before the previous tile's body (NI pieces + RW P loads a tile):
+        // hq(t) and P(t)
+        __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI + RW));
         ll_lds_barrier();
-        LL_TS(ts1);
-        tile_body(stage(t), stage(t + 2), rslot(t + 1), rslot(t + 3), t, puse, pnew);
-        LL_TS(ts2);
-#if LL_STAMP
-        stamp[0] += ts1 - ts0;
-        stamp[3] += ts2 - ts1;
-        stamp[6] += 1;
-#endif
-        (void)ts0, (void)ts1, (void)ts2;
+        tile_body(stage(t), stage(t + 2), t, use, nw);
     };
-    for (int t = t0; t < t1; t += 3) {
-        tile(t, R1, R0);
-        if (t + 1 < t1) tile(t + 1, R2, R1);
-        if (t + 2 < t1) tile(t + 2, R0, R2);
+    for (int t = t0; t < t1; t += 4) {
+        tile(t, R0, R3);
+        if (t + 1 < t1) tile(t + 1, R1, R0);
+        if (t + 2 < t1) tile(t + 2, R2, R1);
+        if (t + 3 < t1) tile(t + 3, R3, R2);
     }
-#if LL_STAMP
-    if (lane == 0 && blockIdx.x * 4 + wave < (1 << 12))
-        for (int k = 0; k < 8; ++k) g_ll_stamps[(1 << 15) + (blockIdx.x * 4 + wave) * 8 + k] = stamp[k];
-#endif
 #pragma unroll
     for (int hh = 0; hh < RW; ++hh)
 #pragma unroll
@@ -1488,7 +1404,7 @@ __global__ __launch_bounds__(256) void k_lmloss_dw_reduce(const float* part, int
 static TuneKnob g_ll_splits{0};  // tuning "lmloss_splits" (0 = auto)
 static TuneKnob g_ll_tsplit{0};  // tuning "lmloss_dw_tsplit" (0 = auto)
 // tuning "lmloss_dw": 0 auto (= 4 where the caller's buffers hold the saved P — the PPO entries
-// given trlx_ppo_loss_from_hidden_workspace_bytes, the *_savep drop-in pair — else 1), 1 the
+// given trlx_ppo_loss_from_hidden_workspace_bytes, the *_ex drop-in pair with a saved region — else 1), 1 the
 // recompute plan (k_lmloss_dw: Sᵀ recomputed, 4 MFMA passes), 4 the saved-P plan (k_lmloss_dwp:
 // 3 passes).  The round-5 H-sliced forms (2, 3) and the 32x32 pair forward (lmloss_fwd = 1) were
 // measured slower and removed (git history keeps them; DESIGN.md §3 lists the measurements).
@@ -1540,7 +1456,7 @@ struct LlWs {
     int* flags;
     float* dwpart;
     uint16_t* pbuf;  // saved-P plan only
-    f32x4_t* prec;
+    uint16_t* hq;
 };
 // Compute units of the current device (the grid plans below).
 static int ll_ncu() {
@@ -1581,13 +1497,17 @@ static LlDwPlan ll_dw_plan(int64_t V, int vpw = kLLTokBlock, int parts = 1) {
 static int ll_pntt(int64_t N) { return int(2 * ((N + kLLTokBlock - 1) / kLLTokBlock)); }
 // the saved P tiles (⌈V/64⌉ x 2⌈N/64⌉ x 4 KB: 0.62 GB at C2) and the per-(split, token) records
 static size_t ll_pbuf_bytes(int64_t N, int64_t V) { return size_t((V + 63) / 64) * ll_pntt(N) * 4096; }
-static size_t ll_prec_bytes(int64_t N) { return size_t(kLLMaxSplits) * N * 16; }
+static size_t ll_hq_bytes(int64_t N, int64_t H) { return size_t(kLLMaxSplits) * N * H * 2; }
+static size_t ll_erec_bytes(int64_t N) { return size_t(kLLMaxSplits) * N * 4; }
+// the dwp kernel addresses hq rows through a 32-bit buffer resource (ll_check's bound)
+static bool ll_hq_fits(int64_t N, int64_t H) { return int64_t(ll_hq_bytes(N, H)) < kLLMaxSpan; }
 
 // Workspace carve-up for N tokens (dwpart: the split blocks' fp32 partials).
 //   fwd:  the forward's partials (O, (m, l)) — false for the backward's own workspace
 //   pbuf: the saved P tiles (the PPO entries' saved-P plan)
-//   prec: the dwp kernel's per-(split, token) records (the PPO saved-P plan, every backward)
-static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, bool fwd, bool pbuf, bool prec) {
+//   hq:   the token rows scaled per split that the dwp kernel streams (the PPO saved-P plan,
+//         every backward: 8·N·H·2 B, 75 MB at C2)
+static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, bool fwd, bool pbuf, bool hq) {
     char* p = static_cast<char*>(base);
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -1606,19 +1526,19 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, boo
     t.dwpart = reinterpret_cast<float*>(take(std::max(size_t(dp.nblk) * dp.tsplit * kLLTokBlock,
                                                       size_t(dp2.nblk) * dp2.tsplit * 2 * kLLTokBlock) * H * 4));
     t.pbuf = reinterpret_cast<uint16_t*>(take(pbuf ? ll_pbuf_bytes(N, V) : 0));
-    t.prec = reinterpret_cast<f32x4_t*>(take(prec ? ll_prec_bytes(N) : 0));
+    t.hq = reinterpret_cast<uint16_t*>(take(hq ? ll_hq_bytes(N, H) : 0));
     if (w) *w = t;
     return off;
 }
-// The drop-in pair's saved region (trlx_lmhead_logprobs_fwd_savep -> _bwd_savep): the P tiles
-// and the forward's g-free records {e^(m_split − lse), 1 − p_y, y, 0}, alive from the forward
-// to the backward (the forward's O partials are not).
-static size_t ll_saved_carve(void* base, int64_t N, int64_t V, uint16_t** pbuf, f32x4_t** prec) {
+// The drop-in pair's saved region (trlx_lmhead_logprobs_fwd_ex -> _bwd_ex): the P tiles (label
+// entries patched) and the per-(split, token) scales e', alive from the forward to the backward
+// (the forward's O partials are not).
+static size_t ll_saved_carve(void* base, int64_t N, int64_t V, uint16_t** pbuf, float** erec) {
     char* p = static_cast<char*>(base);
     const size_t pb = ll_align(ll_pbuf_bytes(N, V));
     if (pbuf) *pbuf = reinterpret_cast<uint16_t*>(p);
-    if (prec) *prec = reinterpret_cast<f32x4_t*>(p ? p + pb : nullptr);
-    return pb + ll_align(ll_prec_bytes(N));
+    if (erec) *erec = reinterpret_cast<float*>(p ? p + pb : nullptr);
+    return pb + ll_align(ll_erec_bytes(N));
 }
 
 static int ll_check(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N, int64_t H,
@@ -1676,11 +1596,11 @@ static int ll_dw(const LmLossArgs& a, hipStream_t s) {
 }
 
 // the common part: shapes, workspace, optional compaction from the mask.  savep: the dW pass
-// reads saved P (its grid plan); fwd / pbuf / prec: the caller's workspace carve (ll_carve)
+// reads saved P (its grid plan); fwd / pbuf / hq: the caller's workspace carve (ll_carve)
 static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N,
                     int64_t H, int64_t V, const int64_t* labels, int64_t lb, const int64_t* compact_mask,
                     void* lm_ws, void* dweight, int dw_dtype, int64_t lddw, LlWs& w, hipStream_t s, bool savep,
-                    bool fwd, bool pbuf, bool prec) {
+                    bool fwd, bool pbuf, bool hq) {
     int rc = ll_check(hidden, ldh, weight, ldw, N, H, V);
     if (rc) return rc;
     TRLX_REQUIRE(labels && lm_ws, TRLX_ERR_ARG, "NULL labels / workspace");
@@ -1701,11 +1621,11 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.dw_full = dp.full;
     a.tsplit = dp.tsplit;
     a.dw_nblk = dp.nblk;
-    ll_carve(lm_ws, N, H, V, &w, fwd, pbuf, prec);
+    ll_carve(lm_ws, N, H, V, &w, fwd, pbuf, hq);
     a.dwpart = w.dwpart;
     a.pbuf = pbuf ? w.pbuf : nullptr;
     a.pntt = ll_pntt(N);
-    a.prec = prec ? w.prec : nullptr;
+    a.hq = hq ? w.hq : nullptr;
     a.opart = w.opart;
     a.mlpart = w.mlpart;
     a.trec = w.trec;
@@ -1757,7 +1677,7 @@ extern "C" int64_t trlx_lmhead_savep_bytes(int64_t N, int64_t H, int64_t V) {
 
 // The saved-P plan runs when the tuning allows it and the caller's workspace holds the P tiles.
 static bool ll_savep_plan(int64_t N, int64_t H, int64_t V, int64_t lm_bytes) {
-    return (g_ll_dw == 0 || g_ll_dw == 4) &&
+    return (g_ll_dw == 0 || g_ll_dw == 4) && ll_hq_fits(N, H) &&
            lm_bytes >= int64_t(ll_carve(nullptr, N, H, V, nullptr, true, true, true));
 }
 
@@ -1879,7 +1799,7 @@ extern "C" int trlx_ppo_loss_from_hidden_split(
 }
 
 // The drop-in autograd pair (lm_head.py): forward -> lp, lse, E; backward -> dh, dW.  The
-// *_savep forms keep the forward's bf16 P tiles in the caller's `saved` region
+// *_ex forms keep the forward's bf16 P tiles in the caller's `saved` region
 // (trlx_lmhead_savep_bytes) so the backward's dW pass reads them back (k_lmloss_dwp, 3 MFMA
 // passes in all) instead of recomputing S (k_lmloss_dw, 4).
 static int ll_dropin_fwd(const void* hidden, int64_t ldh, const void* weight, int64_t ldw, int64_t N, int64_t H,
@@ -1893,7 +1813,7 @@ static int ll_dropin_fwd(const void* hidden, int64_t ldh, const void* weight, in
     int rc = ll_setup(a, hidden, ldh, weight, ldw, N, H, V, labels, lb, mask, lm_workspace, nullptr, TRLX_F32, H,
                       w, s, saved != nullptr, true, false, false);
     if (rc) return rc;
-    if (saved) ll_saved_carve(saved, N, V, &a.pbuf, &a.prec);  // the forward stores P; the combine its records
+    if (saved) ll_saved_carve(saved, N, V, &a.pbuf, &a.erec);  // the forward stores P; the combine e' and the label patch
     a.mode = kLLFwd;
     a.lp = lp_out;
     a.lp_dtype = lp_dtype;
@@ -1919,18 +1839,18 @@ static int ll_dropin_bwd(const void* hidden, int64_t ldh, const void* weight, in
     TRLX_REQUIRE(dh_dtype == TRLX_BF16 || dh_dtype == TRLX_F32, TRLX_ERR_DTYPE, "dhidden dtype");
     TRLX_REQUIRE(dw_dtype == TRLX_BF16 || dw_dtype == TRLX_F32, TRLX_ERR_DTYPE, "dweight dtype");
     TRLX_REQUIRE(lddh % 4 == 0 && lddh >= H && lddw >= H, TRLX_ERR_STRIDE, "gradient row strides");
-    const bool savep = saved != nullptr && dweight != nullptr;
+    // the saved-P dW pass where the forward kept P (and the scaled rows fit the 2-GB addressing);
+    // else the recompute plan, which needs nothing from the forward but lse and E
+    const bool savep = saved != nullptr && dweight != nullptr && ll_hq_fits(N, H) && g_ll_dw != 1;
     // the forward's compaction again (launch_order is a stable, deterministic order: the same
     // compact token indices as the forward's records)
     int rc = ll_setup(a, hidden, ldh, weight, ldw, N, H, V, labels, lb, mask, lm_workspace, dweight, dw_dtype, lddw,
                       w, s, savep, false, false, true);
     if (rc) return rc;
-    if (savep) {  // the forward's P and g-free records in; the g-scaled records (w.prec) out
-        f32x4_t* src = nullptr;
-        ll_saved_carve(const_cast<void*>(saved), N, V, &a.pbuf, &src);
-        a.psrc = src;
+    if (savep) {  // the forward's P and e' in; the scaled h rows (w.hq) out
+        ll_saved_carve(const_cast<void*>(saved), N, V, &a.pbuf, &a.erec);
     } else {
-        a.prec = nullptr;
+        a.hq = nullptr;
     }
     a.mode = kLLBwd;
     a.gin = grad;
