@@ -84,7 +84,7 @@ const char* trlx_last_error(void);
  *                       removed forms 1, 3, 4 are rejected with TRLX_ERR_ARG)
  *   "lmloss_dw"         fused loss dW plan: 0 auto (saved P where the caller's buffers hold it),
  *                       1 = recompute S (k_lmloss_dw), 4 = saved P (k_lmloss_dwp); 2, 3 rejected
- *   "lmloss_dwp_rw"     saved-P dW rows per wave: 0 auto (= 2: 32 rows x H/2), 1 = 16 rows x H
+ *   "lmloss_dwp_form"   saved-P dW blocking: 0 auto (= 2: 32 rows a wave x H/2), 1 = 16 rows a wave x H
  *   "store_policy"      gradient-row store cache policy: 0 auto (default: nt; sc1 for all-VGPR rows
  *                       launches writing > 1.5 GB), 1 none, 2 sc1, 3 sc0|sc1, 4 nt|sc1, 5 nt
  * Results are identical up to fp32 summation order; only speed changes. */

@@ -116,7 +116,9 @@ struct LmLossArgs {
     // blocks are split tsplit ways over the tokens into fp32 partials ([j][vpw][H]) that
     // k_lmloss_dw_reduce sums in split order (the last, partial round of workgroups)
     int dw_full, tsplit, dw_nblk;
-    int dw_vpw;      // vocab rows per dW workgroup (64; the saved-P plan's RW = 2 form: 128)
+    int dw_vpw;      // vocab rows per dW vocab block (64; the saved-P plan: 64·RW of its form)
+    int dw_hsp;      // workgroups per dW vocab block (the saved-P form's hidden parts)
+    int sgran;       // vocab tiles per split granule (ll_split_t0): the dW vocab block's, >= 4
     float* dwpart;
     // saved-P plan (k_lmloss_dwp): the forward stores its bf16 P tiles in the dW kernel's layout
     // (ll_p_store); the combine overwrites each token's label entry with −(1 − p_y)/e' and writes
@@ -323,15 +325,16 @@ __device__ __forceinline__ int ll_fwd_splits(const LmLossArgs& a, int ntb) {
     return best;
 }
 
-// Vocab tiles of split s: [ll_split_t0(s), ll_split_t0(s + 1)), whole 4-tile (128-row) granules,
-// so a saved-P dW workgroup's 128 vocab rows never straddle two splits (its four waves share one
-// staged tile of the split's scaled h); the largest split is at most 3 tiles over the even share.
-__device__ __forceinline__ int ll_split_t0(int s, int nvt, int nsplit) {
-    return min(nvt, 4 * int(int64_t(s) * ((nvt + 3) >> 2) / nsplit));
+// Vocab tiles of split s: [ll_split_t0(s), ll_split_t0(s + 1)), whole granules of `gran` tiles
+// (a.sgran: the saved-P dW vocab block, 128 or 256 rows), so a dW workgroup's vocab rows never
+// straddle two splits (its four waves share one staged tile of the split's scaled h); the largest
+// split is at most gran − 1 tiles over the even share.
+__device__ __forceinline__ int ll_split_t0(int s, int nvt, int nsplit, int gran) {
+    return min(nvt, gran * int(int64_t(s) * ((nvt + gran - 1) / gran) / nsplit));
 }
-__device__ __forceinline__ int ll_split_of(int vt, int nvt, int nsplit) {
+__device__ __forceinline__ int ll_split_of(int vt, int nvt, int nsplit, int gran) {
     int s = 0;
-    for (int k = 1; k < nsplit; ++k) s = ll_split_t0(k, nvt, nsplit) <= vt ? k : s;
+    for (int k = 1; k < nsplit; ++k) s = ll_split_t0(k, nvt, nsplit, gran) <= vt ? k : s;
     return s;
 }
 // The scale of split s's P for a token: e' = e^(m_s − lse) (a split with no vocab: 0), clamped to
@@ -472,7 +475,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     const char* sxr = smem + 3 * kStage + (wave ^ 1) * 4096 + 16 * (lane & 63);
     char* sxw = pscr + 16 * (lane & 63);
     const int nvt = (a.V + kLLRows - 1) / kLLRows;
-    const int t0 = ll_split_t0(split, nvt, nsplit), t1 = ll_split_t0(split + 1, nvt, nsplit);
+    const int t0 = ll_split_t0(split, nvt, nsplit, a.sgran), t1 = ll_split_t0(split + 1, nvt, nsplit, a.sgran);
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
     auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
@@ -914,7 +917,7 @@ __global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
 #pragma unroll
         for (int s = 0; s < kLLMaxSplits; ++s) es[s] = s < nsplit ? ll_scale(ml[s].x, lse) : 0.0f;
         if (a.pbuf && d4 == 0 && yok) {
-            const int nvt = (a.V + kLLRows - 1) / kLLRows, sy = ll_split_of(int(y) >> 5, nvt, nsplit);
+            const int nvt = (a.V + kLLRows - 1) / kLLRows, sy = ll_split_of(int(y) >> 5, nvt, nsplit, a.sgran);
             float ey = es[0];
 #pragma unroll
             for (int s = 1; s < kLLMaxSplits; ++s) ey = sy == s ? es[s] : ey;
@@ -1204,6 +1207,11 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
     }
 }
 
+// A 16-B buffer load: uniform resource and offset, per-lane offset (no 64-bit address register)
+__device__ __forceinline__ s16x8_t ll_buf_load16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(s16x8_t, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
 // ------------------------------------------------------------------ dW from the saved P
 // dW = Σ_t dS_t·h_t with dS = (y == v) ? g·(1 − p_y) : −g·e^(m_split − lse)·P, regrouped so the
 // dW kernel does no arithmetic on its operands: the forward left every bf16 P tile in HBM in this
@@ -1221,8 +1229,11 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dw(LmLossArgs a) {
 // granules), so the four waves share each staged hq tile.  3-stage hq ring (the DMA of tile t+2
 // during tile t) and counted vmcnt: the barrier waits only for what was issued before the
 // previous tile.
+// transposed hq fragments in flight: 2 reads each, and lgkmcnt counts to 15 only — at 8 (16
+// reads + the next fragment's) hipcc could not express the wait for the oldest and drained the
+// whole LDS queue (lgkmcnt(0)) at every tile's first MFMA
 #ifndef LL_DWP_PFO
-#define LL_DWP_PFO 8  // transposed hq fragments in flight
+#define LL_DWP_PFO 6
 #endif
 #ifndef LL_DWP_PIECE_GAP
 #define LL_DWP_PIECE_GAP 4
@@ -1246,7 +1257,8 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     const int g = lane >> 4, c = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
     const int nv = a.rows ? *a.nrows : a.N;
     constexpr int vpw = 64 * RW;
-    const int hp = HSP == 1 ? 0 : int(blockIdx.x) & 1, bid = int(blockIdx.x) / HSP;
+    // the block and hidden part of this workgroup (the parts adjacent in dispatch order)
+    const int hp = HSP == 1 ? 0 : int(blockIdx.x) % HSP, bid = int(blockIdx.x) / HSP;
     const bool part = bid >= a.dw_full;
     const int j = bid - a.dw_full;
     const int vb = part ? a.dw_full + j / a.tsplit : bid;
@@ -1256,7 +1268,7 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
     // the vocab split of the workgroup's rows (the forward's plan, ll_fwd_splits / ll_split_t0)
     const int nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
-    const int sp = ll_split_of((vb * vpw) >> 5, (a.V + kLLRows - 1) / kLLRows, nsplit);
+    const int sp = ll_split_of((vb * vpw) >> 5, (a.V + kLLRows - 1) / kLLRows, nsplit, a.sgran);
     // transposed reads of the hq tile: rows 8g + 4hf + q, columns 16nb + 4p (the subtile image)
     int trb8[2][2];
 #pragma unroll
@@ -1273,30 +1285,32 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
         const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         return __builtin_bit_cast(bf16x8_t, v);
     };
-    // hq rows [nsplit][N][H]: the host keeps nsplit·N·H·2 below the 2 GB sentinel (ll_hq_fits)
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.hq, uint32_t(int64_t(nsplit) * a.N * H * 2));
-    const int hrow0 = sp * a.N;  // hq row of compact token 0 of this split
+    // this split's hq rows [N][H] of the live tokens only (ll_hq_fits keeps the whole buffer
+    // below the 2 GB sentinel): rows past the live count read as zeros (out of range)
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.hq + int64_t(sp) * a.N * H, uint32_t(nv) * (H * 2));
     auto stage = [&](int t) __attribute__((always_inline)) { return smem + (t % 3) * kStage; };
     // piece il of the part's image = piece hp·HC/16 + il of the full-H image (a multiple of 8:
-    // the same rows); tokens past the live count read as zero rows (out of range)
+    // the same rows): the lane's offset within a tile (loop-invariant) plus the tile's (uniform);
+    // past the token split's last tile an out-of-range offset (fetches nothing).  Issued
+    // unconditionally — a branch around it would leave hipcc unable to count the loads in flight
+    // across the loop and it would wait for all of them (vmcnt(0)) instead of the counted waits
     auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
-        const int il = wave + G::kWaves * k, i = hp * (HC / 16) + il;
-        const int m = t * kLLRows + ll_piece_row(il, lane);
-        const int off = ll16_piece_src(i, (hrow0 + m) * (H * 2), lane);
+        const int il = wave + G::kWaves * k;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + il * 1024), 16,
-                                                 t < t1 && m < nv ? off : int(0x7ffff000), 0, 0, 0);
+                                                 t < t1 ? ll16_piece_src(hp * (HC / 16) + il, ll_piece_row(il, lane) * (H * 2), lane) + t * (kLLRows * H * 2)
+                                                        : int(0x7ffff000), 0, 0,
+                                                 0);
     };
     // P chunk of tile t for row half hh (rows r0 + 16hh + c, tokens 8g..8g+7), clamped to the
-    // split's last tile: 64-row block (r0 + 16hh) / 64, dW wave slot ((r0 + 16hh) / 16) & 3
-    const s16x8_t* pbase[RW];
-#pragma unroll
-    for (int hh = 0; hh < RW; ++hh) {
-        const int rr0 = r0 + 16 * hh;
-        pbase[hh] = reinterpret_cast<const s16x8_t*>(a.pbuf) + (int64_t(rr0 >> 6) * a.pntt * 4 + ((rr0 >> 4) & 3)) * 64 +
-                    lane;
-    }
+    // split's last tile: 64-row block (r0 + 16hh) / 64, dW wave slot ((r0 + 16hh) / 16) & 3.  A
+    // uniform base plus the lane's 16 B: no per-tile address register (a temporary that reused a
+    // P destination made hipcc wait for the previous tile's P loads every fourth tile)
+    const __amdgpu_buffer_rsrc_t rp =
+        make_rsrc(reinterpret_cast<const char*>(a.pbuf) + (int64_t(r0 >> 6) * a.pntt * 4 + ((r0 >> 4) & 3)) * 1024,
+                  uint32_t(a.pntt) * 4096u);  // this block's token tiles (128·N B)
+    const int plane = 16 * lane;
     auto load_p = [&](int t, int hh) __attribute__((always_inline)) {
-        return pbase[hh][int64_t(min(t, t1 - 1)) * 256];
+        return ll_buf_load16(rp, plane, min(t, t1 - 1) * 4096 + 1024 * hh);
     };
     f32x4_t D[RW][DB];  // dW[r0 + 16hh + 4g + r][16nb + c]
 #pragma unroll
@@ -1346,12 +1360,16 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
         }
     };
     auto tile = [&](int t, const s16x8_t (&use)[RW], s16x8_t (&nw)[RW]) __attribute__((always_inline)) {
-        // everything issued before the previous tile's body (NI pieces + RW P loads a tile):
+        // everything issued before the previous tile's body (RW P loads + NI pieces a tile):
         // hq(t) and P(t)
         __builtin_amdgcn_s_waitcnt(ll_vmcnt(NI + RW));
         ll_lds_barrier();
         tile_body(stage(t), stage(t + 2), t, use, nw);
     };
+    // (tiles 2-4 of a group conditional: unconditional groups padded with empty tiles, or a
+    // 1-3 tile tail after the loop, spared hipcc's wait analysis a conservative vmcnt at each
+    // group's first MFMA but made it rotate the dW accumulators between registers every tile —
+    // ~40 moves a tile, 3-4 % slower: profiles/r06e_dwp_loop_ab.log)
     for (int t = t0; t < t1; t += 4) {
         tile(t, R0, R3);
         if (t + 1 < t1) tile(t + 1, R1, R0);
@@ -1409,19 +1427,20 @@ static TuneKnob g_ll_tsplit{0};  // tuning "lmloss_dw_tsplit" (0 = auto)
 // 3 passes).  The round-5 H-sliced forms (2, 3) and the 32x32 pair forward (lmloss_fwd = 1) were
 // measured slower and removed (git history keeps them; DESIGN.md §3 lists the measurements).
 static TuneKnob g_ll_dw{0};
-// tuning "lmloss_dwp_rw": the saved-P dW kernel's vocab rows per wave, 16·RW (0 auto = 2, 1, 2)
-static TuneKnob g_ll_rw{0};
+// tuning "lmloss_dwp_form": the saved-P dW kernel's blocking, vocab rows per wave 16·RW x hidden
+// parts (workgroups per vocab block): 0 auto (= 2), 1 = RW 1 / whole H, 2 = RW 2 / H halves
+static TuneKnob g_ll_form{0};
 
 int lmloss_set_tuning(const char* key, int64_t value, bool* handled) {
     const bool sp = key && !__builtin_strcmp(key, "lmloss_splits");
     const bool ts = key && !__builtin_strcmp(key, "lmloss_dw_tsplit");
     const bool fw = key && !__builtin_strcmp(key, "lmloss_fwd");
     const bool dwk = key && !__builtin_strcmp(key, "lmloss_dw");
-    const bool rwk = key && !__builtin_strcmp(key, "lmloss_dwp_rw");
+    const bool rwk = key && !__builtin_strcmp(key, "lmloss_dwp_form");
     *handled = sp || ts || fw || dwk || rwk;
     if (rwk) {
-        TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "lmloss_dwp_rw: 0 auto, 1, 2");
-        g_ll_rw = int(value);
+        TRLX_REQUIRE(value >= 0 && value <= 2, TRLX_ERR_ARG, "lmloss_dwp_form: 0 auto, 1, 2");
+        g_ll_form = int(value);
         return TRLX_OK;
     }
     if (fw) {  // one forward form is built: the 16x16x32 one (0 / 2 select it)
@@ -1472,13 +1491,28 @@ static int ll_ncu() {
     return ncu;
 }
 
+// The saved-P dW forms (tuning "lmloss_dwp_form"; 0 = the default, kLLDwpForm): vocab rows per
+// block (64·RW), hidden parts (workgroups per block) and workgroups per CU.  The recompute plan's
+// k_lmloss_dw is form 1's shape (64 rows x H).
+// Measured and dropped (round 6, profiles/r06f_dwp_forms_*.jsonl, interleaved, whole update): RW 2
+// with 256 hidden columns a workgroup and two workgroups per CU (+3 % C2, +4 % C3), RW 4 with 256
+// columns (+1 % / +2 %), and the hidden parts of a block back to back on one XCD (±0.3 %).
+struct LlDwForm {
+    int rw, hsp, vpw;
+};
+constexpr int kLLDwpForm = 2;
+static LlDwForm ll_dw_form(int f, int64_t H) {
+    (void)H;
+    return f == 1 ? LlDwForm{1, 1, 64} : LlDwForm{2, 2, 128};
+}
+
 // dW grid plan: whole rounds of workgroups own a vocab block each; the blocks of the last,
 // partial round are split over the tokens so that round is (nearly) full instead of a tail of
 // a few long workgroups (C2: 786 blocks on 256 CUs = 3 rounds + 18 blocks, the 18 split 14 ways).
 struct LlDwPlan {
     int full, tsplit, nblk;  // workgroups = full + nblk·tsplit
 };
-// parts: workgroups per vocab block (the saved-P RW = 2 form's two hidden halves)
+// parts: workgroups per vocab block (the saved-P forms' hidden parts)
 static LlDwPlan ll_dw_plan(int64_t V, int vpw = kLLTokBlock, int parts = 1) {
     const int ncu = std::max(1, ll_ncu() / parts);
     const int nvb = int((V + vpw - 1) / vpw);
@@ -1522,9 +1556,13 @@ static size_t ll_carve(void* base, int64_t N, int64_t H, int64_t V, LlWs* w, boo
     t.order = reinterpret_cast<int*>(take(size_t(N + 4) * 4));
     t.cnt = reinterpret_cast<int*>(take(size_t(order_chunks(N) + 1) * 4));
     t.flags = reinterpret_cast<int*>(take(size_t((N + kLLRows - 1) / kLLRows) * kLLMaxSplits * 4 * 4));  // 4 waves a workgroup
-    const LlDwPlan dp = ll_dw_plan(V), dp2 = ll_dw_plan(V, 2 * kLLTokBlock, 2);  // 64- / 128-row blocks
-    t.dwpart = reinterpret_cast<float*>(take(std::max(size_t(dp.nblk) * dp.tsplit * kLLTokBlock,
-                                                      size_t(dp2.nblk) * dp2.tsplit * 2 * kLLTokBlock) * H * 4));
+    size_t dwp = 0;  // the largest token-split partial buffer over the dW forms
+    for (int f = 1; f <= 2; ++f) {
+        const LlDwForm fm = ll_dw_form(f, H);
+        const LlDwPlan d = ll_dw_plan(V, fm.vpw, fm.hsp);
+        dwp = std::max(dwp, size_t(d.nblk) * d.tsplit * fm.vpw);
+    }
+    t.dwpart = reinterpret_cast<float*>(take(dwp * H * 4));
     t.pbuf = reinterpret_cast<uint16_t*>(take(pbuf ? ll_pbuf_bytes(N, V) : 0));
     t.hq = reinterpret_cast<uint16_t*>(take(hq ? ll_hq_bytes(N, H) : 0));
     if (w) *w = t;
@@ -1579,10 +1617,12 @@ template <class G>
 static int ll_launch_dw(const LmLossArgs& a, hipStream_t s) {
     const dim3 grid(unsigned(a.dw_full + a.dw_nblk * a.tsplit));
     if (a.pbuf) {
-        if (a.dw_vpw == 2 * kLLTokBlock)  // 128 rows x H/2 per workgroup: two per vocab block
-            hipLaunchKernelGGL((k_lmloss_dwp<G, 2, 2>), dim3(2 * grid.x), dim3(G::kThreads), 0, s, a);
+        // HSP workgroups per vocab block
+        const unsigned gx = grid.x * unsigned(a.dw_hsp);
+        if (a.dw_hsp == 1)
+            hipLaunchKernelGGL((k_lmloss_dwp<G, 1, 1>), dim3(gx), dim3(G::kThreads), 0, s, a);
         else
-            hipLaunchKernelGGL((k_lmloss_dwp<G, 1, 1>), grid, dim3(G::kThreads), 0, s, a);
+            hipLaunchKernelGGL((k_lmloss_dwp<G, 2, 2>), dim3(gx), dim3(G::kThreads), 0, s, a);
         return check_launch("k_lmloss_dwp");
     }
     hipLaunchKernelGGL(k_lmloss_dw<G>, grid, dim3(G::kThreads), 0, s, a);
@@ -1616,8 +1656,13 @@ static int ll_setup(LmLossArgs& a, const void* hidden, int64_t ldh, const void* 
     a.nsplit = g_ll_splits ? g_ll_splits : kLLMaxSplits;
     a.nsplit_fixed = g_ll_splits != 0;
     a.ncu = ll_ncu();
-    a.dw_vpw = savep && g_ll_rw != 1 ? 2 * kLLTokBlock : kLLTokBlock;
-    const LlDwPlan dp = ll_dw_plan(V, a.dw_vpw, a.dw_vpw / kLLTokBlock);
+    const LlDwForm fm = ll_dw_form(savep ? (g_ll_form ? int(g_ll_form) : kLLDwpForm) : 1, H);
+    a.dw_vpw = fm.vpw;
+    a.dw_hsp = savep ? fm.hsp : 1;
+    // split granules of the dW vocab block (>= 4 tiles: the drop-in forward and backward agree
+    // whatever the plan; the tuning must not change between them)
+    a.sgran = std::max(4, fm.vpw / kLLRows);
+    const LlDwPlan dp = ll_dw_plan(V, fm.vpw, a.dw_hsp);
     a.dw_full = dp.full;
     a.tsplit = dp.tsplit;
     a.dw_nblk = dp.nblk;
