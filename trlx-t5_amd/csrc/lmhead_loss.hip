@@ -329,8 +329,8 @@ __device__ __forceinline__ int ll_fwd_splits(const LmLossArgs& a, int ntb) {
 // (a.sgran: the saved-P dW vocab block, 128 or 256 rows), so a dW workgroup's vocab rows never
 // straddle two splits (its four waves share one staged tile of the split's scaled h); the largest
 // split is at most gran − 1 tiles over the even share.
-__device__ __forceinline__ int ll_split_t0(int s, int nvt, int nsplit, int gran) {
-    return min(nvt, gran * int(int64_t(s) * ((nvt + gran - 1) / gran) / nsplit));
+__device__ __forceinline__ int ll_split_t0(int s, int nvt, int nsplit, int gran) {  // 32-bit: s·ngr < 2^31
+    return min(nvt, gran * int(unsigned(s) * unsigned((nvt + gran - 1) / gran) / unsigned(nsplit)));
 }
 __device__ __forceinline__ int ll_split_of(int vt, int nvt, int nsplit, int gran) {
     int s = 0;
@@ -476,16 +476,20 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     char* sxw = pscr + 16 * (lane & 63);
     const int nvt = (a.V + kLLRows - 1) / kLLRows;
     const int t0 = ll_split_t0(split, nvt, nsplit, a.sgran), t1 = ll_split_t0(split + 1, nvt, nsplit, a.sgran);
-    const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w, uint32_t(int64_t(a.V) * a.ldw * 2));
+    // the split's W rows only [32·t0, min(V, 32·t1)): rows past V and tiles past the split read
+    // as zeros by the range check (no per-piece select), offsets relative to the split's first row
+    const __amdgpu_buffer_rsrc_t rw =
+        make_rsrc(a.w + int64_t(t0) * kLLRows * a.ldw,
+                  uint32_t(max(0, min(a.V, t1 * kLLRows) - t0 * kLLRows)) * uint32_t(a.ldw) * 2u);
+    const int tbytes = kLLRows * int(a.ldw) * 2;  // one tile of W rows
     auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
-        const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
-        ll16_piece(slot, i, rw, t < t1 ? off : int(0x7ffff000), lane);
+        ll16_piece(slot, i, rw, (t - t0) * tbytes + ll_piece_row(i, lane) * int(a.ldw) * 2, lane);
     };
     auto load_piece = [&](int t, int k) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
-        const int off = (t * kLLRows + ll_piece_row(i, lane)) * int(a.ldw) * 2;
-        return __builtin_amdgcn_raw_buffer_load_b128(rw, ll16_piece_src(i, t < t1 ? off : int(0x7ffff000), lane), 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(
+            rw, ll16_piece_src(i, (t - t0) * tbytes + ll_piece_row(i, lane) * int(a.ldw) * 2, lane), 0, 0);
     };
     const int rb = ll16_rb(lane);
     const int trb[2] = {ll16_trb(lane, 0), ll16_trb(lane, 1)};
