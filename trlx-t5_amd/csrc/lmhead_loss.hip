@@ -178,6 +178,21 @@ __device__ __forceinline__ int ll16_piece_src(int i, int row_bytes, int lane) {
     const int ch = 4 * (2 * (i & 1) + (lane >> 5)) + ((lane & 3) ^ ll16_swz((r >> 2) & 3));
     return row_bytes + (i >> 3) * 256 + ch * 16;
 }
+// The buffer resource of 32-row tile t of a [rows][ld] bf16 matrix, limited to its rows below
+// `nrows` (0: none): rows past it read as zeros by the range check, so a piece's per-lane offset
+// within the tile is loop-invariant and the tile is scalar arithmetic only.  (A helper, not a
+// lambda in the kernel body: hipcc's host pass dropped the kernels' launch stubs for a lambda
+// returning a resource, and the library then linked with undefined symbols.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ll_tile_rsrc(const uint16_t* base, int ld, int t, int nrows) {
+    // (the clamp compiles to a VALU v_med3: readfirstlane keeps the resource in scalar registers —
+    // a resource in vector registers makes hipcc wrap the load in a waterfall loop)
+    const int rows = __builtin_amdgcn_readfirstlane(max(0, min(kLLRows, nrows - t * kLLRows)));
+    return make_rsrc(base + int64_t(t) * kLLRows * ld, uint32_t(rows) * uint32_t(ld) * 2u);
+}
+__device__ __forceinline__ void ll16_piece_at(char* slot, int il, __amdgpu_buffer_rsrc_t rs, int off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + il * 1024), 16, off, 0, 0,
+                                             0);
+}
 __device__ __forceinline__ void ll16_piece(char* slot, int i, __amdgpu_buffer_rsrc_t rs, int row_bytes, int lane) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + i * 1024), 16,
                                              ll16_piece_src(i, row_bytes, lane), 0, 0, 0);
@@ -476,20 +491,18 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     char* sxw = pscr + 16 * (lane & 63);
     const int nvt = (a.V + kLLRows - 1) / kLLRows;
     const int t0 = ll_split_t0(split, nvt, nsplit, a.sgran), t1 = ll_split_t0(split + 1, nvt, nsplit, a.sgran);
-    // the split's W rows only [32·t0, min(V, 32·t1)): rows past V and tiles past the split read
-    // as zeros by the range check (no per-piece select), offsets relative to the split's first row
-    const __amdgpu_buffer_rsrc_t rw =
-        make_rsrc(a.w + int64_t(t0) * kLLRows * a.ldw,
-                  uint32_t(max(0, min(a.V, t1 * kLLRows) - t0 * kLLRows)) * uint32_t(a.ldw) * 2u);
-    const int tbytes = kLLRows * int(a.ldw) * 2;  // one tile of W rows
+    // one buffer resource per W tile: its rows [32t, min(V, 32t + 32)), none past the split — rows
+    // past V and tiles past the split read as zeros by the range check, and a piece's per-lane
+    // offset is loop-invariant: the tile is all scalar arithmetic (no VALU per piece)
     auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
-        ll16_piece(slot, i, rw, (t - t0) * tbytes + ll_piece_row(i, lane) * int(a.ldw) * 2, lane);
+        ll16_piece(slot, i, ll_tile_rsrc(a.w, int(a.ldw), t, t < t1 ? a.V : 0), ll_piece_row(i, lane) * int(a.ldw) * 2,
+                   lane);
     };
     auto load_piece = [&](int t, int k) __attribute__((always_inline)) {
         const int i = wave + G::kWaves * k;
-        return __builtin_amdgcn_raw_buffer_load_b128(
-            rw, ll16_piece_src(i, (t - t0) * tbytes + ll_piece_row(i, lane) * int(a.ldw) * 2, lane), 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(ll_tile_rsrc(a.w, int(a.ldw), t, t < t1 ? a.V : 0),
+                                                     ll16_piece_src(i, ll_piece_row(i, lane) * int(a.ldw) * 2, lane), 0, 0);
     };
     const int rb = ll16_rb(lane);
     const int trb[2] = {ll16_trb(lane, 0), ll16_trb(lane, 1)};
@@ -1259,7 +1272,10 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, c = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
-    const int nv = a.rows ? *a.nrows : a.N;
+    // the live token count, uniform (readfirstlane tells hipcc so: the tile resources below
+    // derive from it, and a resource in vector registers makes it wrap every buffer load in a
+    // waterfall loop)
+    const int nv = __builtin_amdgcn_readfirstlane(a.rows ? *a.nrows : a.N);
     constexpr int vpw = 64 * RW;
     // the block and hidden part of this workgroup (the parts adjacent in dispatch order)
     const int hp = HSP == 1 ? 0 : int(blockIdx.x) % HSP, bid = int(blockIdx.x) / HSP;
@@ -1271,8 +1287,9 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
     const int ntt = (nv + kLLRows - 1) / kLLRows;
     const int t0 = int(int64_t(ts) * ntt / nts), t1 = int(int64_t(ts + 1) * ntt / nts);
     // the vocab split of the workgroup's rows (the forward's plan, ll_fwd_splits / ll_split_t0)
-    const int nsplit = ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock);
-    const int sp = ll_split_of((vb * vpw) >> 5, (a.V + kLLRows - 1) / kLLRows, nsplit, a.sgran);
+    // (ll_fwd_splits' float arithmetic runs on the VALU: readfirstlane keeps the split uniform)
+    const int nsplit = __builtin_amdgcn_readfirstlane(ll_fwd_splits(a, (nv + kLLTokBlock - 1) / kLLTokBlock));
+    const int sp = __builtin_amdgcn_readfirstlane(ll_split_of((vb * vpw) >> 5, (a.V + kLLRows - 1) / kLLRows, nsplit, a.sgran));
     // transposed reads of the hq tile: rows 8g + 4hf + q, columns 16nb + 4p (the subtile image)
     int trb8[2][2];
 #pragma unroll
@@ -1289,21 +1306,20 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
         const s16x8_t v = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         return __builtin_bit_cast(bf16x8_t, v);
     };
-    // this split's hq rows [N][H] of the live tokens only (ll_hq_fits keeps the whole buffer
-    // below the 2 GB sentinel): rows past the live count read as zeros (out of range)
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc(a.hq + int64_t(sp) * a.N * H, uint32_t(nv) * (H * 2));
+    // one buffer resource per hq tile: this split's rows of the tile's live tokens [32t, min(nv,
+    // 32t + 32)), none past the token split — the rest read as zeros by the range check, and a
+    // piece's per-lane offset is loop-invariant: the tile is all scalar arithmetic (ll_hq_fits
+    // keeps the whole hq buffer below the 2 GB sentinel)
+    const uint16_t* hq0 = a.hq + int64_t(sp) * a.N * H;
     auto stage = [&](int t) __attribute__((always_inline)) { return smem + (t % 3) * kStage; };
     // piece il of the part's image = piece hp·HC/16 + il of the full-H image (a multiple of 8:
-    // the same rows): the lane's offset within a tile (loop-invariant) plus the tile's (uniform);
-    // past the token split's last tile an out-of-range offset (fetches nothing).  Issued
-    // unconditionally — a branch around it would leave hipcc unable to count the loads in flight
-    // across the loop and it would wait for all of them (vmcnt(0)) instead of the counted waits
+    // the same rows).  Issued unconditionally — a branch around it would leave hipcc unable to
+    // count the loads in flight across the loop and it would wait for all of them (vmcnt(0))
+    // instead of the counted waits
     auto issue_piece = [&](int t, char* slot, int k) __attribute__((always_inline)) {
         const int il = wave + G::kWaves * k;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, (__attribute__((address_space(3))) void*)(slot + il * 1024), 16,
-                                                 t < t1 ? ll16_piece_src(hp * (HC / 16) + il, ll_piece_row(il, lane) * (H * 2), lane) + t * (kLLRows * H * 2)
-                                                        : int(0x7ffff000), 0, 0,
-                                                 0);
+        ll16_piece_at(slot, il, ll_tile_rsrc(hq0, H, t, t < t1 ? nv : 0),
+                      ll16_piece_src(hp * (HC / 16) + il, ll_piece_row(il, lane) * (H * 2), lane));
     };
     // P chunk of tile t for row half hh (rows r0 + 16hh + c, tokens 8g..8g+7), clamped to the
     // split's last tile: 64-row block (r0 + 16hh) / 64, dW wave slot ((r0 + 16hh) / 16) & 3.  A
