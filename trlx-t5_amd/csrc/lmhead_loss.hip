@@ -388,6 +388,13 @@ __device__ __forceinline__ uint16_t* ll_p_elem(const LmLossArgs& a, int v, int m
 #ifndef LL_FWD_PSTAGE_GAP
 #define LL_FWD_PSTAGE_GAP 30
 #endif
+// the softmax's gaps in the S loop (see kSM0 below): first gap and stride of the exps
+#ifndef LL_FWD_SM0
+#define LL_FWD_SM0 12
+#endif
+#ifndef LL_FWD_SMS
+#define LL_FWD_SMS 3
+#endif
 // O exchange (default): the O product splits the hidden columns over the four waves instead of
 // the tokens — wave w accumulates d blocks 16i + 4w + j (i < H/256, j < 4) for all 64 tokens of
 // the workgroup, each transposed W fragment feeding four MFMAs (one per token block) — so a wave
@@ -430,7 +437,14 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     auto piece_at = [](int k) { return k >= kPO && (k - kPO) % kPG == 0 && (k - kPO) / kPG < NI; };
     // SAVEP: the gap (of the S + O sequence) that stages P through LDS (after the pack at 11;
     // with LL_FWD_SPAIR the O loop's first gap instead)
-    constexpr int kPS = LL_FWD_PSTAGE_GAP;
+    // softmax(t) in the S loop's gaps: the token max at kSM0, the offset / overflow flag two gaps
+    // later, the exps one every kSMS gaps from kSM0 + 3 (the 8th with the row sum and the bf16 pack
+    // at kSMP), P(t) to the exchange slot at kSMP + 1
+    // (the macros are for H = 768's 48 gaps; scaled to the S loop's gaps at other H)
+    constexpr int kSM0 = LL_FWD_SM0 * NG / 48, kSMS = LL_FWD_SMS * NG / 48 > 0 ? LL_FWD_SMS * NG / 48 : 1;
+    constexpr int kSMP = kSM0 + 3 + 7 * kSMS;
+    constexpr int kPS = LL_FWD_PSTAGE_GAP * NG / 48 > kSMP + 1 ? LL_FWD_PSTAGE_GAP * NG / 48 : kSMP + 2;
+    static_assert(kSMS >= 1 && kSMP + 1 < 2 * KS, "the softmax gaps inside the S loop");
     static_assert(kPS > 11 && kPS < NG + DB, "the P staging gap");
     static_assert(NG >= 20, "the P-save gaps");
     constexpr bool OX = LL_FWD_OXCH;
@@ -452,7 +466,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     char* xch = pscr + 2048 + 16 * (lane & 63);
     const char* xrd = smem + 3 * kStage + 2048 + 16 * (lane & 63);
     constexpr bool PSL = OX && LL_FWD_PSLOT;  // the saved-P transpose from the exchange slot
-    static_assert(!PSL || kPS > 12, "the saved-P transpose after the exchange slot's write (gap 12)");
+    static_assert(!PSL || kPS > kSMP + 1, "the saved-P transpose after the exchange slot's write");
     auto p_stage = [&](const bf16x8_t& pbv) __attribute__((always_inline)) {
         if constexpr (PSL)
             return ll_p_stage_slot(pscr + 2048, lane);
@@ -652,20 +666,22 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                     pt = p_stage(pb);  // PSL: after the slot write at gap 12
                 }
             }
-            if (k == 0) {  // the lane's max + token max (no mask inside the loop: see ll_fwd_block)
+            if (k == kSM0) {  // the lane's max + token max (no mask inside the loop: the last tile's own path)
                 const float lm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])),
                                        fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
                 m4 = ll_rows_max(lm);
-            } else if (k == 2) {
+            } else if (k == kSM0 + 2) {
                 sm_chunk(1, t, std::false_type{});
-            } else if (k >= 3 && k < 11) {
-                sm_chunk(k - 1, t, std::false_type{});
-            } else if (k == 11) {
+            } else if (k == kSMP) {
+                sm_chunk(9, t, std::false_type{});
                 sm_chunk(10, t, std::false_type{});
                 pb = pack8(pr);
-            } else if (OX && k == 12) {
+            } else if (OX && k == kSMP + 1) {
                 *reinterpret_cast<bf16x8_t*>(xch) = pb;  // the exchange: read after the S loop's barrier
             }
+#pragma unroll
+            for (int e = 0; e < 7; ++e)
+                if (k == kSM0 + 3 + kSMS * e) sm_chunk(2 + e, t, std::false_type{});
             if (kFill == 0 && piece_at(k) && !(kLLAblate & 2048)) issue_piece(t + 2, fut, (k - kPO) / kPG);
             if (kFill == 2 && piece_at(k)) ldv[(k - kPO) / kPG] = load_piece(t + 2, (k - kPO) / kPG);
             if (OX && k >= NG - PFX) tfx[k - (NG - PFX)] = ox_frag(cur, k - (NG - PFX));
