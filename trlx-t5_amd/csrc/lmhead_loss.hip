@@ -450,6 +450,20 @@ __device__ __forceinline__ uint16_t* ll_p_elem(const LmLossArgs& a, int v, int m
 #ifndef LL_FWD_FILL
 #define LL_FWD_FILL 0
 #endif
+// MFMAs carried across a barrier (O exchange + S pair split): the last LL_FWD_DEFO W^T fragments of
+// O(t) (4 MFMAs each) issue after step t+1's first barrier, the last LL_FWD_DEFS MFMAs of S(t+1)
+// after step t's exchange barrier, behind the LDS reads each barrier releases (the W rows of tile
+// t+1 / the exchanged P), so the matrix pipe runs while those reads are in flight
+#ifndef LL_FWD_DEFO
+#define LL_FWD_DEFO 1
+#endif
+#ifndef LL_FWD_DEFS
+#define LL_FWD_DEFS 4
+#endif
+// the S loop gap that adds the partner's partial of S(t) (read after the step's first barrier)
+#ifndef LL_FWD_XRG
+#define LL_FWD_XRG 4
+#endif
 // SAVEP with the O exchange: the saved-P transpose read from the exchange slot (ll_p_stage_slot)
 #ifndef LL_FWD_PSLOT
 #define LL_FWD_PSLOT 1
@@ -573,16 +587,41 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     // (the first PFX fragments come in tf: read before the exchange barrier, they depend on the
     // tile only)
     constexpr int PFX = 2;
-    auto ox_product = [&](const char* tile, bf16x8_t (&tf)[OF], int gbase, auto&& gap) __attribute__((always_inline)) {
-        bf16x8_t px[4];
+    constexpr int DEFO = OX && SP ? LL_FWD_DEFO : 0, DEFS = OX && SP ? LL_FWD_DEFS : 0;
+    static_assert(DEFO >= 0 && DEFO < OF - PFX && DEFS >= 0 && DEFS <= 8, "carried MFMAs");
+    // the exchanged P of the four token blocks (held past the step for the carried O fragments)
+    bf16x8_t px[4], tfd[DEFO > 0 ? DEFO : 1];
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb) px[tb] = bf16x8_t{};
+#pragma unroll
+    for (int i = 0; i < (DEFO > 0 ? DEFO : 1); ++i) tfd[i] = bf16x8_t{};
+    // the carried O MFMAs (zero operands before the first step)
+    auto o_carried = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < DEFO; ++i)
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb)
+                O[4 * (OF - DEFO + i) + tb] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(tfd[i], px[tb], O[4 * (OF - DEFO + i) + tb], 0, 0, 0);
+    };
+    // NF: the fragments done here (OF, or OF − DEFO with the rest carried); pre: after the P reads
+    auto ox_product = [&](const char* tile, bf16x8_t (&tf)[OF], int gbase, auto&& gap, auto&& pre, auto nf_tag)
+                          __attribute__((always_inline)) {
+        constexpr int NF = decltype(nf_tag)::value;
 #pragma unroll
         for (int tb = 0; tb < 4; ++tb) px[tb] = *reinterpret_cast<const bf16x8_t*>(xrd + 4096 * tb);
+        pre();
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int f = 0; f < OF; ++f) {
             if (f + PFX < OF) tf[f + PFX] = ox_frag(tile, f + PFX);
+            if (f < NF) {
 #pragma unroll
-            for (int tb = 0; tb < 4; ++tb)
-                O[4 * f + tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[f], px[tb], O[4 * f + tb], 0, 0, 0);
+                for (int tb = 0; tb < 4; ++tb)
+                    O[4 * f + tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tf[f], px[tb], O[4 * f + tb], 0, 0, 0);
+            } else {
+                tfd[f - NF] = tf[f];
+            }
             gap(gbase + f);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -672,8 +711,13 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             for (int k = 0; k < PF; ++k) af[k] = ll16_row_frag(nx, rb, k / KS, k % KS);
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e)  // S(t) for the softmax; S(t+1) accumulates anew
-            x[e] = SP ? s[e >> 2][e & 3] + xr[e >> 2][e & 3] : s[e >> 2][e & 3];
+        for (int e = 0; e < 8; ++e)  // S(t) for the softmax (SP: + the partner's, at gap LL_FWD_XRG); S(t+1) anew
+            x[e] = s[e >> 2][e & 3];
+        if constexpr (DEFO > 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            o_carried();  // O(t-1)'s last fragments, behind the reads of tile t+1
+            __builtin_amdgcn_sched_barrier(0);
+        }
         s[0] = f32x4_t{};
         s[1] = f32x4_t{};
         so[0] = f32x4_t{};
@@ -689,7 +733,11 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             } else if (k + PF < NG) {
                 af[k + PF] = ll16_row_frag(nx, rb, (k + PF) / KS, (k + PF) % KS);
             }
-            s_mfma(nx, af, k);
+            if (SP && k == LL_FWD_XRG) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x[e] += xr[e >> 2][e & 3];
+            }
+            if (k < NG - DEFS) s_mfma(nx, af, k);
             if (SAVEP && (!SP || PSL) && k == kPS) {
                 if (kLLAblate & 64) {  // diagnostic: no LDS round trip (wrong layout)
                     pt = __builtin_bit_cast(s16x8_t, pb);
@@ -731,7 +779,10 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                 if (SAVEP && kPSt > 0 && f == kPSt && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);
                 if (kFill == 1 && !(kLLAblate & 2048)) issue_piece(t + 2, fut, f);
                 if (kFill == 2) *reinterpret_cast<vec4u*>(fut + (wave + G::kWaves * f) * 1024 + 16 * lane) = ldv[f];
-            });
+            }, [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int k = NG - DEFS; k < NG; ++k) s_mfma(nx, af, k);  // S(t+1)'s last, behind the P reads
+            }, std::integral_constant<int, OF - DEFO>{});
         } else {
         // ---- O(t): tr reads of tile t's W (cur) | MFMA
         constexpr int PFO = 4;
@@ -796,6 +847,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             c1 = c2;
             c2 = cc;
         }
+        o_carried();  // the last step's carried O fragments
         // the last tile: its (masked) softmax and O product
         if constexpr (SP) {
             ll_lds_barrier();  // the partner's partial of the last tile; every wave done with the P exchange
@@ -812,7 +864,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
             bf16x8_t tfx[OF];
 #pragma unroll
             for (int f = 0; f < PFX; ++f) tfx[f] = ox_frag(c0, f);
-            ox_product(c0, tfx, 0, [](int) {});
+            ox_product(c0, tfx, 0, [](int) {}, []() {}, std::integral_constant<int, OF>{});
         } else {
 #pragma unroll
             for (int nb = 0; nb < DB; ++nb)
