@@ -460,6 +460,11 @@ __device__ __forceinline__ uint16_t* ll_p_elem(const LmLossArgs& a, int v, int m
 #ifndef LL_FWD_DEFS
 #define LL_FWD_DEFS 4
 #endif
+// O exchange: W^T fragments in flight in the O loop (2 reads each; the first ones read in the S
+// loop's last gaps)
+#ifndef LL_FWD_PFX
+#define LL_FWD_PFX 2
+#endif
 // the S loop gap that adds the partner's partial of S(t) (read after the step's first barrier)
 #ifndef LL_FWD_XRG
 #define LL_FWD_XRG 4
@@ -586,7 +591,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     // OX: O(t) over the wave's d groups for the four token blocks, after the exchange barrier
     // (the first PFX fragments come in tf: read before the exchange barrier, they depend on the
     // tile only)
-    constexpr int PFX = 2;
+    constexpr int PFX = LL_FWD_PFX;
     constexpr int DEFO = OX && SP ? LL_FWD_DEFO : 0, DEFS = OX && SP ? LL_FWD_DEFS : 0;
     static_assert(DEFO >= 0 && DEFO < OF - PFX && DEFS >= 0 && DEFS <= 8, "carried MFMAs");
     // the exchanged P of the four token blocks (held past the step for the carried O fragments)
