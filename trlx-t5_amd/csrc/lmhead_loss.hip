@@ -313,42 +313,16 @@ __device__ __forceinline__ s16x8_t ll_p_stage_slot(const char* slot, int lane) {
     const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(rd + 64));
     return s16x8_t{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 }
-#ifndef LL_FWD_PSTORE
-#define LL_FWD_PSTORE 0
-#endif
-#ifndef LL_FWD_OPART_NT
-#define LL_FWD_OPART_NT 0
-#endif
-#ifndef LL_DWP_OUT_NT
-#define LL_DWP_OUT_NT 0
-#endif
-// the forward's O partials (read once, by the combine)
-__device__ __forceinline__ void ll_st_f4(f32x4_t* p, f32x4_t v) {
-    if (LL_FWD_OPART_NT)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
-template <class T>
-__device__ __forceinline__ void ll_st_out(T* p, T v) {  // the dW kernel's output
-    if (LL_DWP_OUT_NT)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
-#ifndef LL_FWD_PSTORE_NT
-#define LL_FWD_PSTORE_NT 1
-#endif
+// P is stored non-temporal: 2·N·V bytes written once and read once, by k_lmloss_dwp after the
+// combine (C2 update −7 %, profiles/r06n_fwd_pstore_nt_ab.log; nt on the O partials and on dW's
+// output measured neutral, r06o_opart_dwout_nt_ab.log)
 __device__ __forceinline__ void ll_p_store(const LmLossArgs& a, const s16x8_t& v, int t, int tt, int half,
                                            int lane) {
     const int g = lane >> 4, c = lane & 15;
     char* dst = reinterpret_cast<char*>(a.pbuf) +
                 ((int64_t(t >> 1) * a.pntt + tt) * 4 + 2 * (t & 1) + (g >> 1)) * 1024 +
                 16 * (16 * (2 * half + (g & 1)) + c);
-    if (LL_FWD_PSTORE_NT)
-        __builtin_nontemporal_store(v, reinterpret_cast<s16x8_t*>(dst));
-    else
-        *reinterpret_cast<s16x8_t*>(dst) = v;
+    __builtin_nontemporal_store(v, reinterpret_cast<s16x8_t*>(dst));
 }
 
 // Vocab splits of the forward for ntb live token blocks: the count (<= a.nsplit) whose last
@@ -492,8 +466,6 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
     constexpr int kSM0 = LL_FWD_SM0 * NG / 48, kSMS = LL_FWD_SMS * NG / 48 > 0 ? LL_FWD_SMS * NG / 48 : 1;
     constexpr int kSMP = kSM0 + 3 + 7 * kSMS;
     constexpr int kPS = LL_FWD_PSTAGE_GAP * NG / 48 > kSMP + 1 ? LL_FWD_PSTAGE_GAP * NG / 48 : kSMP + 2;
-    // the saved-P store: in the O loop's gap kPSt (0: after the O loop)
-    constexpr int kPSt = LL_FWD_PSTORE;
     static_assert(kSMS >= 1 && kSMP + 1 < 2 * KS, "the softmax gaps inside the S loop");
     static_assert(kPS > 11 && kPS < NG + DB, "the P staging gap");
     static_assert(NG >= 20, "the P-save gaps");
@@ -781,7 +753,6 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                 // same region (the partner read the last one before the exchange barrier)
                 if (SP && SAVEP && !PSL && f == 0) pt = ll_p_stage(pscr, pb, lane);
                 if (SP && f == 1) sx_write();
-                if (SAVEP && kPSt > 0 && f == kPSt && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);
                 if (kFill == 1 && !(kLLAblate & 2048)) issue_piece(t + 2, fut, f);
                 if (kFill == 2) *reinterpret_cast<vec4u*>(fut + (wave + G::kWaves * f) * 1024 + 16 * lane) = ldv[f];
             }, [&]() __attribute__((always_inline)) {
@@ -805,7 +776,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
         }
         }
         static_assert(kPG * (NI - 1) + kPO < NG + DB, "every DMA piece before the P store (the step's counted wait)");
-        if (SAVEP && (kPSt == 0 || !OX) && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);
+        if (SAVEP && !(kLLAblate & 32)) ll_p_store(a, pt, t, ptt, phalf, lane);  // after the O loop
         LL_TS(ts3);
 #if LL_STAMP
         stamp[0] += ts1 - ts0;
@@ -899,7 +870,7 @@ __device__ __forceinline__ void ll_fwd16_block(const LmLossArgs& a, char* smem, 
                 float* op = a.opart + (int64_t(split) * a.N + tmb) * a.H + 64 * wave + 4 * g;
 #pragma unroll
                 for (int f = 0; f < OF; ++f)
-                    ll_st_f4(reinterpret_cast<f32x4_t*>(op + 256 * (f >> 2) + 16 * (f & 3)), O[4 * f + tb]);
+                    *reinterpret_cast<f32x4_t*>(op + 256 * (f >> 2) + 16 * (f & 3)) = O[4 * f + tb];
             }
         }
         if (valid && g == 0) a.mlpart[int64_t(split) * a.N + tm] = make_float2(mrun, lt);
@@ -1509,17 +1480,17 @@ __global__ __launch_bounds__(256, 1) void k_lmloss_dwp(LmLossArgs a) {
             if (part) {
                 float* out = a.dwpart + (int64_t(j) * vpw + vr) * H + hp * HC + c;
 #pragma unroll
-                for (int nb = 0; nb < DB; ++nb) ll_st_out(out + 16 * nb, D[hh][nb][r]);
+                for (int nb = 0; nb < DB; ++nb) out[16 * nb] = D[hh][nb][r];
             } else if (v < a.V) {
                 const int64_t o = int64_t(v) * a.lddw + hp * HC + c;
                 if (a.dw_dtype == TRLX_F32) {
                     float* out = static_cast<float*>(a.dw) + o;
 #pragma unroll
-                    for (int nb = 0; nb < DB; ++nb) ll_st_out(out + 16 * nb, D[hh][nb][r]);
+                    for (int nb = 0; nb < DB; ++nb) out[16 * nb] = D[hh][nb][r];
                 } else {
                     uint16_t* out = static_cast<uint16_t*>(a.dw) + o;
 #pragma unroll
-                    for (int nb = 0; nb < DB; ++nb) ll_st_out(out + 16 * nb, f2bf(D[hh][nb][r]));
+                    for (int nb = 0; nb < DB; ++nb) out[16 * nb] = f2bf(D[hh][nb][r]);
                 }
             }
         }
