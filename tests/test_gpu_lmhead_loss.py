@@ -370,6 +370,28 @@ def test_lm_head_logprobs_plans_agree_and_frozen_operands():
     assert _rel(a[1], dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
 
 
+def test_lm_head_logprobs_saved_p_released_by_backward():
+    """The saved-P region (2·N·V bytes) lives in the autograd node's saved tensors: the backward
+    releases it with them while the caller still holds lp (its grad_fn alive), and a
+    retain_graph backward keeps it for a second pass with the same gradients."""
+    N, H, V = 257, 768, 4099
+    h, w, y = _operands(N, H, V, 23)
+    wg = w.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(h.to(DEV), wg, y.to(DEV), out_dtype=torch.float32, plan="saved_p")
+    saved = lp.grad_fn.saved_tensors
+    nbytes = P._lib.query("trlx_lmhead_savep_bytes", N, H, V)
+    assert saved[-1] is not None and saved[-1].numel() == nbytes
+    del saved
+    lp.sum().backward(retain_graph=True)
+    g1 = wg.grad.clone()
+    wg.grad = None
+    lp.sum().backward()  # the second pass reads the same P region
+    torch.cuda.synchronize()
+    assert torch.equal(wg.grad, g1)
+    with pytest.raises(RuntimeError):
+        lp.grad_fn.saved_tensors  # freed with the graph, lp still referenced
+
+
 @pytest.mark.parametrize("plan", ["saved_p", "recompute"])
 @pytest.mark.parametrize("N,H,V", [(300, 768, 5000), (6144, 768, 32128), (77, 512, 1031)])
 def test_lm_head_logprobs_mask_compacts(plan, N, H, V):

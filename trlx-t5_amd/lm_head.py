@@ -74,15 +74,17 @@ class _LmHeadLogprobs(torch.autograd.Function):
                   y.data_ptr(), 1, _lib.ptr(mask), lp.data_ptr(), _lib.dtype_code(lp), lse.data_ptr(), e.data_ptr(),
                   ws.data_ptr(), _lib.ptr(saved), _lib.stream_of(h))
         del ws  # the forward's partials: free once the combine has run (stream-ordered)
-        ctx.save_for_backward(h, w, y, lse, e)
+        # the P region rides save_for_backward, so autograd frees it with the graph's other saved
+        # tensors once the backward has run (not when the last reference to lp goes); the
+        # backward only reads it, so a retain_graph second backward sees the same bytes
+        ctx.save_for_backward(h, w, y, lse, e, saved)
         ctx.mask = mask
-        ctx.saved_p = saved  # raw bytes the backward only reads (a second backward sees the same)
         ctx.shapes = (hidden.shape, hidden.dtype, weight.shape, weight.dtype)
         return lp.view(labels.shape)
 
     @staticmethod
     def backward(ctx, grad_lp):
-        h, w, y, lse, e = ctx.saved_tensors
+        h, w, y, lse, e, saved_p = ctx.saved_tensors
         hshape, hdt, wshape, wdt = ctx.shapes
         N, H, V = h.shape[0], h.shape[1], w.shape[0]
         dev = h.device
@@ -98,7 +100,7 @@ class _LmHeadLogprobs(torch.autograd.Function):
         dh = torch.empty((N, H), dtype=hdt, device=dev) if need_h else None
         dw = torch.empty((V, H), dtype=wdt, device=dev) if need_w else None
         ws = torch.empty(_lib.query("trlx_lmhead_loss_bwd_workspace_bytes", N, H, V), dtype=torch.uint8, device=dev)
-        saved = ctx.saved_p if need_w else None
+        saved = saved_p if need_w else None
         _lib.call("trlx_lmhead_logprobs_bwd_ex", h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), N, H, V,
                   y.data_ptr(), 1, _lib.ptr(ctx.mask), g.data_ptr(), _lib.dtype_code(g), lse.data_ptr(), e.data_ptr(),
                   _lib.ptr(dh), H if dh is None else dh.stride(0), _lib.dtype_code(dh if dh is not None else dw),
