@@ -136,7 +136,8 @@ def _oracle_loss_side(x, lp_old, adv_w, ret, mask):
 
 @pytest.mark.parametrize("B,T,V,H,masked", [(4, 9, 1031, 768, False), (16, 48, 32128, 768, True),
                                             (128, 48, 50257, 768, False), (256, 48, 32128, 768, True),
-                                            (8, 20, 5000, 512, True)])
+                                            (8, 20, 5000, 512, True), (1, 3, 1031, 768, False),
+                                            (3, 2, 777, 512, True)])
 def test_hot_path_loss_from_hidden_vs_oracle(B, T, V, H, masked):
     """PPOHotPath.step_from_hidden (fused experience lm_head + GAE, then the fused loss side)
     against the oracle's loss side on the product's own experience outputs (lp_old, whitened
@@ -418,6 +419,39 @@ def test_lm_head_logprobs_mask_compacts(plan, N, H, V):
     with torch.no_grad():
         lp_ng = P.lm_head_logprobs(h.to(DEV), w.to(DEV), y.to(DEV), out_dtype=torch.float32, mask=m.to(DEV))
     torch.testing.assert_close(lp_ng, lp.detach(), rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("plan", ["saved_p", "recompute"])
+@pytest.mark.parametrize("N,H,V,live", [(1, 768, 1000, "all"), (1, 512, 50257, "all"), (130, 768, 4099, "one"),
+                                        (130, 768, 4099, "none"), (64, 512, 33, "none")])
+def test_lm_head_logprobs_edge_token_counts(plan, N, H, V, live):
+    """Edge token counts of the fused loss side: a single token (one partial 64-token block, one
+    32-token tile of P), a single live token among masked ones, and every token masked (no live
+    token block: the forward, combine and dW passes see nv = 0) — lp / dh / dW against fp64 of
+    the live rows, and exact zeros where nothing is live (dW included, never NaN)."""
+    h, w, y = _operands(N, H, V, N + V + 7)
+    gout = torch.randn(N, generator=torch.Generator().manual_seed(N + 1))
+    m = torch.ones(N, dtype=torch.long)
+    if live == "one":
+        m.zero_()
+        m[N // 2] = 1
+    elif live == "none":
+        m.zero_()
+    hd = h.to(DEV).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    lp = P.lm_head_logprobs(hd, wg, y.to(DEV), out_dtype=torch.float32, plan=plan,
+                            mask=None if live == "all" else m.to(DEV))
+    (lp * gout.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(hd.grad).all() and torch.isfinite(wg.grad).all()
+    keep = m.bool()
+    assert (lp.detach().cpu()[~keep] == 0).all() and (hd.grad.cpu()[~keep] == 0).all()
+    if not keep.any():
+        assert (wg.grad == 0).all()
+        return
+    lp64, dh64, dw64 = _fp64_grads(h[keep], w, y[keep], gout[keep])
+    torch.testing.assert_close(lp.detach()[keep.to(DEV)].double(), lp64, rtol=1e-5, atol=2e-5)
+    assert _rel(hd.grad[keep.to(DEV)], dh64) < 1e-2 and _rel(wg.grad, dw64) < 1e-2
 
 
 def test_lm_head_logprobs_auto_plan_falls_back_when_p_does_not_fit(monkeypatch):
