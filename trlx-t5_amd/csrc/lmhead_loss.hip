@@ -918,8 +918,10 @@ __global__ __launch_bounds__(G::kThreads, 1) void k_lmloss_fwd(LmLossArgs a) {
 // (m, l) first — they depend on m only, splits past nsplit re-read the last one and are weighted
 // 0 — then the label row, and the PPO scalars, which every thread reads (same addresses) so
 // that each computes g itself and no second barrier broadcasts it.
+// 8 waves a SIMD (≤ 64 VGPRs): one more wave of loads in flight than the 65 registers hipcc picks
+// by itself allow (−3.5 µs of ~50 at C2, profiles/r06w8_combine_occupancy_kab.log)
 template <int MODE>
-__global__ __launch_bounds__(256) void k_lmloss_combine(LmLossArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_lmloss_combine(LmLossArgs a) {
     const int m = blockIdx.x, d4 = threadIdx.x;
     __shared__ float s_tok[4];
     int row = m;
